@@ -1,0 +1,102 @@
+"""Load the golden fixtures written by tests/golden/make_golden.py (allow_pickle=False)."""
+
+from __future__ import annotations
+
+import glob
+import json
+import os
+import sys
+
+import numpy as np
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, GOLDEN_DIR)
+from inputs import make_inputs, make_masks  # noqa: E402,F401
+
+PARAM_NAMES = (
+    "temporal.0.weight", "temporal.1.weight", "temporal.1.bias", "spatial.weight",
+    "aggregation.0.weight", "aggregation.0.bias", "block_2.0.weight", "block_2.1.weight",
+    "block_2.2.weight", "block_2.2.bias", "classifier.weight", "classifier.bias",
+)
+
+
+def fixture_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+
+
+class Golden:
+    def __init__(self, name: str):
+        z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
+        self.z = {k: z[k] for k in z.files}
+        self.meta = json.loads(str(self.z["meta"]))
+        m = self.meta
+        self.x, self.y = make_inputs(m["B"], m["C"], m["T"], m["seed"])
+
+    def group(self, prefix: str) -> dict:
+        n = len(prefix) + 1
+        return {k[n:]: v for k, v in self.z.items() if k.startswith(prefix + ".")}
+
+    @property
+    def init(self):
+        return self.group("init")
+
+    def init_params(self):
+        s = self.init
+        return {k: s[k] for k in PARAM_NAMES}
+
+    def init_buffers(self):
+        return {k: v for k, v in self.init.items() if k not in PARAM_NAMES}
+
+    def masks(self, step=0):
+        m = self.meta
+        if m["p"] == 0:
+            return None
+        return make_masks(m["B"], m["F1"] * m["D"], m["T"], m["seed"] * 100 + step, m["p"])
+
+
+# BN1's affine parameters are (near-)invisible to the loss: BN2 (model.py:47) renormalises the
+# spatial conv output, which is linear in BN1's output (model.py:32 -> 34).  d(beta1) is exactly 0
+# and d(gamma1) is O(bn_eps / var2) in exact arithmetic; the reference's fp32 values are dominated
+# by rounding residue (|g| ~ 5e-7 against ~1e-2 for the other grads).  They are compared with an
+# absolute tolerance scaled by the largest gradient of the whole model instead of their own.
+NEAR_ZERO_GRADS = ("temporal.1.weight", "temporal.1.bias")
+
+
+def assert_grads_close(actual: dict, expected: dict, rtol=1e-4, atol_frac=1e-5, prefix=""):
+    gmax = max(float(np.max(np.abs(np.asarray(v)))) for v in expected.values())
+    for k in PARAM_NAMES:
+        if k in NEAR_ZERO_GRADS:
+            assert_close(actual[k], expected[k], rtol=rtol, atol_abs=atol_frac * gmax,
+                         name=prefix + k)
+        else:
+            assert_close(actual[k], expected[k], rtol=rtol, atol_frac=atol_frac, name=prefix + k)
+
+
+def assert_params_close(actual: dict, expected: dict, steps=1, lr=1e-3, rtol=1e-5, atol_frac=1e-5,
+                        prefix=""):
+    """Post-Adam parameters.  Adam normalises each element's step (|step| <= ~lr), so rounding
+    residue in the NEAR_ZERO_GRADS becomes an O(lr) move of gamma1/beta1 whose sign is noise in
+    the reference itself; those two are held to |diff| <= 2*lr*steps (the loss does not see them)."""
+    for k in PARAM_NAMES:
+        if k in NEAR_ZERO_GRADS:
+            assert_close(actual[k], expected[k], rtol=0.0, atol_abs=2.0 * lr * steps,
+                         name=prefix + k)
+        else:
+            assert_close(actual[k], expected[k], rtol=rtol, atol_frac=atol_frac, name=prefix + k)
+
+
+def assert_close(actual, expected, rtol=1e-4, atol_frac=1e-5, name="", atol_abs=None):
+    """SURVEY 8(c) tolerance: rtol 1e-4 with atol = 1e-5 * max|ref| (grads near zero)."""
+    a = np.asarray(actual, dtype=np.float64)
+    e = np.asarray(expected, dtype=np.float64)
+    assert a.shape == e.shape, f"{name}: shape {a.shape} != {e.shape}"
+    atol = atol_frac * max(float(np.max(np.abs(e))) if e.size else 0.0, 1e-30)
+    if atol_abs is not None:
+        atol = atol_abs
+    err = np.abs(a - e)
+    lim = atol + rtol * np.abs(e)
+    bad = err > lim
+    if np.any(bad):
+        i = np.unravel_index(np.argmax(err - lim), e.shape)
+        raise AssertionError(f"{name}: {int(bad.sum())}/{e.size} out of tolerance; worst at {i}: "
+                             f"got {a[i]!r} expected {e[i]!r} (atol {atol:.3g}, rtol {rtol})")

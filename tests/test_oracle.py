@@ -1,0 +1,70 @@
+"""Pin the CPU oracle against the golden vectors produced by the reference."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import (Golden, PARAM_NAMES, assert_close, assert_grads_close,
+                         assert_params_close, fixture_names)
+from oracle import numpy_ref as nr
+from oracle import torch_ref as tr
+
+TRAIN_FIXTURES = [n for n in fixture_names() if n != "G3"]
+
+
+@pytest.mark.parametrize("name", TRAIN_FIXTURES)
+def test_numpy_oracle_first_step(name):
+    g = Golden(name)
+    m = g.meta
+    params, bufs = g.init_params(), g.init_buffers()
+    logits, cache, nb = nr.forward(params, bufs, g.x, train=True, p=m["p"], masks=g.masks(0))
+    assert_close(logits, g.z["logits"], name="logits")
+    loss, dl = nr.cross_entropy(logits, g.y)
+    assert abs(loss - float(g.z["loss"])) <= 1e-5 * max(1.0, abs(loss))
+    grads = nr.backward(cache, dl * m["loss_scale"])
+    assert_grads_close(grads, g.group("grad"), prefix="grad.")
+    for k, v in g.group("buf1").items():
+        assert_close(nb[k], v, name=k)
+    st = nr.adam_init(params)
+    newp = nr.adam_step(params, grads, st)
+    assert_params_close(newp, g.group("step1"), prefix="step1.")
+
+
+def test_numpy_oracle_eval_logits():
+    g = Golden("G3")
+    logits, _, _ = nr.forward(g.init_params(), g.init_buffers(), g.x, train=False)
+    assert_close(logits, g.z["eval_logits"], name="eval_logits")
+
+
+def test_numpy_oracle_trajectory_G7():
+    g = Golden("G7")
+    params, bufs = g.init_params(), g.init_buffers()
+    st = nr.adam_init(params)
+    losses = []
+    for _ in range(g.meta["steps"]):
+        out = nr.train_step(params, bufs, g.x, g.y, st)
+        params, bufs = out["params"], out["buffers"]
+        losses.append(out["loss"])
+    np.testing.assert_allclose(losses, g.z["losses"], rtol=1e-4)
+    assert_params_close(params, g.group("final"), steps=g.meta["steps"], rtol=1e-4, atol_frac=1e-4)
+
+
+def test_clamp_fixture_saturates():
+    """G6 must actually exercise both gradient clamps (model.py:44,84)."""
+    g = Golden("G6")
+    assert np.max(np.abs(g.z["grad.spatial.weight"])) == pytest.approx(1.0)
+    assert np.max(np.abs(g.z["grad.classifier.weight"])) == pytest.approx(0.25)
+
+
+@pytest.mark.parametrize("name", ["G1", "G2", "G4", "G5_8x64"])
+def test_torch_oracle_matches_golden(name):
+    g = Golden(name)
+    m = g.meta
+    ref = tr.TorchRefEEGNet(g.init, p=m["p"])
+    opt = tr.make_optimizer(ref)
+    masks = g.masks(0)
+    loss, logits = tr.train_step(ref, opt, torch.from_numpy(g.x), torch.from_numpy(g.y), masks)
+    assert_close(logits.detach().numpy(), g.z["logits"], name="logits")
+    assert_params_close({k: v.detach().numpy() for k, v in ref.params.items()}, g.group("step1"))
