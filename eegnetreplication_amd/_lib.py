@@ -1,0 +1,93 @@
+"""ctypes binding of libeegnet_hip.so (C-ABI declared in include/eegnet_abi.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950).  There is
+no fallback: if the library is missing or a call fails, a RuntimeError says so.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libeegnet_hip.so")
+
+_lock = threading.Lock()
+_lib = None
+
+
+class Dims(ctypes.Structure):
+    """Mirror of ``eegnet_dims`` (include/eegnet_abi.h)."""
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("T", ctypes.c_int),
+        ("F1", ctypes.c_int), ("D", ctypes.c_int), ("K1", ctypes.c_int),
+        ("p_drop", ctypes.c_float), ("bn_eps", ctypes.c_float), ("bn_momentum", ctypes.c_float),
+    ]
+
+
+_vp = ctypes.c_void_p
+_SIGS = {
+    "eegnet_param_count": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(ctypes.c_int64)]),
+    "eegnet_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(ctypes.c_size_t)]),
+    "eegnet_forward_train": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp,
+                                            ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp]),
+    "eegnet_backward": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp, _vp,
+                                       ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
+    "eegnet_forward_eval": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp]),
+    "eegnet_adam_step": (ctypes.c_int, [ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_float,
+                                        ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp]),
+    "eegnet_train_step": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, ctypes.c_uint64,
+                                         ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_float,
+                                         ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
+                                         _vp, _vp]),
+    "eegnet_last_error": (ctypes.c_char_p, []),
+    "eegnet_build_info": (ctypes.c_char_p, []),
+}
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes handle.  Raises RuntimeError when the .so is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(
+                f"libeegnet_hip.so not found at {p}: build it with `python -c 'import "
+                f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). There is no "
+                f"CPU fallback for the EEGNet HIP path.")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().eegnet_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
+
+
+def dims(B, C, T, F1=8, D=2, K1=32, p=0.5, eps=1e-5, momentum=0.1) -> Dims:
+    return Dims(int(B), int(C), int(T), int(F1), int(D), int(K1), float(p), float(eps),
+                float(momentum))
+
+
+def param_count(d: Dims) -> int:
+    out = ctypes.c_int64(0)
+    check(load().eegnet_param_count(ctypes.byref(d), ctypes.byref(out)), "eegnet_param_count")
+    return int(out.value)
+
+
+def workspace_bytes(d: Dims) -> int:
+    out = ctypes.c_size_t(0)
+    check(load().eegnet_workspace_bytes(ctypes.byref(d), ctypes.byref(out)),
+          "eegnet_workspace_bytes")
+    return int(out.value)

@@ -1,0 +1,151 @@
+"""Torch-facing wrappers of the HIP C-ABI: train/eval forward, backward, Adam, fused train step.
+
+Every function here runs the HIP kernels of ``csrc/eegnet_kernels.hip`` through
+``libeegnet_hip.so``; tensors must live on a HIP device.  There is no CPU or eager-PyTorch path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+NCLS = 4
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def require_device(t: torch.Tensor, what: str):
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what} is on '{t.device}': the MI355X EEGNet path runs on a HIP device only "
+            f"(move the model and the inputs to 'cuda').")
+
+
+@dataclass(frozen=True)
+class Shape:
+    """Static dims of one EEGNet instance (model.py:13)."""
+    C: int
+    T: int
+    F1: int = 8
+    D: int = 2
+    K1: int = 32
+    p: float = 0.5
+    eps: float = 1e-5
+    momentum: float = 0.1
+
+    @property
+    def F2(self):
+        return self.F1 * self.D
+
+    @property
+    def T1(self):
+        return self.T // 4
+
+    @property
+    def T2(self):
+        return self.T1 // 8
+
+    def dims(self, B: int, p: float | None = None) -> _lib.Dims:
+        return _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1,
+                         self.p if p is None else p, self.eps, self.momentum)
+
+    def param_shapes(self):
+        """(name, shape) in nn.Module.named_parameters() order (model.py:22-84)."""
+        F1, F2, C, K1 = self.F1, self.F2, self.C, self.K1
+        nf = F2 * (self.T // 32)
+        return [
+            ("temporal.0.weight", (F1, 1, 1, K1)), ("temporal.1.weight", (F1,)),
+            ("temporal.1.bias", (F1,)), ("spatial.weight", (F2, 1, C, 1)),
+            ("aggregation.0.weight", (F2,)), ("aggregation.0.bias", (F2,)),
+            ("block_2.0.weight", (F2, 1, 1, 16)), ("block_2.1.weight", (F2, F2, 1, 1)),
+            ("block_2.2.weight", (F2,)), ("block_2.2.bias", (F2,)),
+            ("classifier.weight", (NCLS, nf)), ("classifier.bias", (NCLS,)),
+        ]
+
+    def n_params(self):
+        n = 0
+        for _, s in self.param_shapes():
+            k = 1
+            for d in s:
+                k *= d
+            n += k
+        return n
+
+    def bn_layout(self):
+        """Flat bn_buffers order of the ABI: rm1, rv1, rm2, rv2, rm3, rv3."""
+        F1, F2 = self.F1, self.F2
+        return [("temporal.1.running_mean", F1), ("temporal.1.running_var", F1),
+                ("aggregation.0.running_mean", F2), ("aggregation.0.running_var", F2),
+                ("block_2.2.running_mean", F2), ("block_2.2.running_var", F2)]
+
+
+def new_workspace(shape: Shape, B: int, device) -> torch.Tensor:
+    nbytes = _lib.workspace_bytes(shape.dims(B))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def forward_train(shape: Shape, flat_params, bn_flat, x, ws, seed: int, offset: int,
+                  masks=None, p: float | None = None) -> torch.Tensor:
+    """Train-mode forward: BN batch stats (+ running-stat update in bn_flat), dropout."""
+    B = x.shape[0]
+    logits = torch.empty((B, NCLS), dtype=torch.float32, device=x.device)
+    m2, m3 = masks if masks is not None else (None, None)
+    d = shape.dims(B, p)
+    _lib.check(_lib.load().eegnet_forward_train(
+        ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(m2), _ptr(m3),
+        ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(logits), _ptr(ws), _stream()),
+        "eegnet_forward_train")
+    return logits
+
+
+def backward(shape: Shape, flat_params, x, ws, seed: int, offset: int, dlogits=None, labels=None,
+             masks=None, p: float | None = None, grads=None, loss=None) -> torch.Tensor:
+    B = x.shape[0]
+    if grads is None:
+        grads = torch.empty_like(flat_params)
+    m2, m3 = masks if masks is not None else (None, None)
+    d = shape.dims(B, p)
+    _lib.check(_lib.load().eegnet_backward(
+        ctypes.byref(d), _ptr(flat_params), _ptr(x), _ptr(dlogits), _ptr(labels), _ptr(m2),
+        _ptr(m3), ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(loss), _ptr(ws),
+        _stream()), "eegnet_backward")
+    return grads
+
+
+def forward_eval(shape: Shape, flat_params, bn_flat, x) -> torch.Tensor:
+    B = x.shape[0]
+    logits = torch.empty((B, NCLS), dtype=torch.float32, device=x.device)
+    d = shape.dims(B)
+    _lib.check(_lib.load().eegnet_forward_eval(
+        ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(logits), _stream()),
+        "eegnet_forward_eval")
+    return logits
+
+
+def adam_step(params, grads, exp_avg, exp_avg_sq, step_i32, lr=1e-3, betas=(0.9, 0.999), eps=1e-7):
+    _lib.check(_lib.load().eegnet_adam_step(
+        ctypes.c_int64(params.numel()), _ptr(params), _ptr(grads), _ptr(exp_avg), _ptr(exp_avg_sq),
+        _ptr(step_i32), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
+        ctypes.c_float(eps), _stream()), "eegnet_adam_step")
+
+
+def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset: int, grads,
+               adam_state, step_i32, ws, loss, logits=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-7,
+               p: float | None = None):
+    """One fused hot-loop iteration (model.py:141-148) on the device, no host sync."""
+    d = shape.dims(x.shape[0], p)
+    _lib.check(_lib.load().eegnet_train_step(
+        ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(labels),
+        ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),
+        _ptr(step_i32), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
+        ctypes.c_float(eps), _ptr(loss), _ptr(logits), _ptr(ws), _stream()), "eegnet_train_step")

@@ -1,0 +1,109 @@
+/*
+ * eegnet_abi.h -- C-ABI of libeegnet_hip.so, the MI355X (gfx950) EEGNet train/infer step.
+ *
+ * Drop-in boundary for the reference's hot path (PraKesEy/EEGNetReplication):
+ *   EEGNet.forward            src/eegnet_repl/model.py:91-99   -> eegnet_forward_train / eegnet_forward_eval
+ *   loss.backward() + hooks   src/eegnet_repl/model.py:44,84,147 -> eegnet_backward
+ *   optimizer.step() (Adam)   src/eegnet_repl/train.py:94-101, model.py:148 -> eegnet_adam_step
+ *   one hot-loop iteration    src/eegnet_repl/model.py:136-148 -> eegnet_train_step
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer (hipMalloc / torch CUDA tensor) unless noted.  The library never
+ *     allocates or frees; the caller owns params, buffers and the workspace (eegnet_workspace_bytes).
+ *   - All work is enqueued on `stream`; no host synchronisation happens inside, so every call can be
+ *     captured in a hipGraph.
+ *   - Return 0 on success, a negative EEGNET_E* code otherwise; eegnet_last_error() (thread-local)
+ *     describes the failure.  The Python side raises RuntimeError with that text.
+ *   - `params` is ONE flat fp32 buffer in nn.Module.named_parameters() order:
+ *       temporal.0.weight[F1,1,1,K1]  temporal.1.weight[F1]  temporal.1.bias[F1]
+ *       spatial.weight[F2,1,C,1]      aggregation.0.weight[F2] aggregation.0.bias[F2]
+ *       block_2.0.weight[F2,1,1,16]   block_2.1.weight[F2,F2,1,1]
+ *       block_2.2.weight[F2]          block_2.2.bias[F2]
+ *       classifier.weight[4,F2*(T/32)] classifier.bias[4]          (F2 = F1*D)
+ *     (1,716 floats for EEGNet-8,2 at C=22, T=256).  `grads` has the same layout.
+ *   - `bn_buffers` is one flat fp32 buffer: running_mean/running_var of temporal.1 [F1,F1],
+ *     aggregation.0 [F2,F2], block_2.2 [F2,F2] (num_batches_tracked stays on the host).
+ *   - x is [B,C,T] fp32 row-major; labels int64 [B] in [0,4); logits fp32 [B,4].
+ *   - Dropout keep-masks: uint8 [B,F2,T/4] and [B,F2,T/128] (1 = keep), nullable.  NULL means the
+ *     on-device counter-based generator keyed by (seed, offset): the same (seed, offset) always
+ *     produces the same masks, and forward and backward see the same ones.
+ */
+#ifndef EEGNET_ABI_H
+#define EEGNET_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct eegnet_dims {
+    int B;          /* trials in the batch                                  */
+    int C;          /* EEG channels          (model.py:13 `C`)              */
+    int T;          /* samples per trial     (model.py:13 `T`)              */
+    int F1;         /* temporal filters      (model.py:13, default 8)       */
+    int D;          /* depth multiplier      (model.py:13, default 2)       */
+    int K1;         /* temporal kernel length (model.py:26: 32; 64 also supported) */
+    float p_drop;   /* dropout p             (model.py:13, 50, 74)          */
+    float bn_eps;   /* BatchNorm2d eps (1e-5)                               */
+    float bn_momentum; /* BatchNorm2d momentum (0.1)                        */
+} eegnet_dims;
+
+enum {
+    EEGNET_OK = 0,
+    EEGNET_EINVAL = -1,   /* unsupported or inconsistent dims / null pointer */
+    EEGNET_ELAUNCH = -2,  /* a kernel launch failed                          */
+};
+
+enum { EEGNET_TRAIN = 1, EEGNET_EVAL = 0 };
+
+/* Number of fp32 elements of the flat parameter buffer for these dims. */
+int eegnet_param_count(const eegnet_dims* dims, int64_t* out);
+
+/* Bytes of scratch the train-mode calls need (forward -> backward state lives here). */
+int eegnet_workspace_bytes(const eegnet_dims* dims, size_t* out);
+
+/* Train-mode forward (BN batch statistics, dropout, running-stat momentum update).
+ * Replaces model.py:141 `preds = model(signals)` in train mode.  Leaves what backward needs in `ws`. */
+int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn_buffers,
+                         const float* x, const uint8_t* mask2, const uint8_t* mask3,
+                         uint64_t seed, uint64_t offset, float* logits, void* ws, void* stream);
+
+/* Backward of the last eegnet_forward_train on the same `ws` (same x, params, masks, seed/offset).
+ * Gradient source: `dlogits` [B,4] if non-NULL (autograd), else mean cross-entropy against `labels`
+ * (train.py:103), in which case the scalar loss is written to `loss` (device fp32, nullable).
+ * `grads` receives all 12 parameter gradients with the clamps of model.py:44 (+-1) and model.py:84
+ * (+-0.25) applied. */
+int eegnet_backward(const eegnet_dims* dims, const float* params, const float* x,
+                    const float* dlogits, const int64_t* labels, const uint8_t* mask2,
+                    const uint8_t* mask3, uint64_t seed, uint64_t offset, float* grads, float* loss,
+                    void* ws, void* stream);
+
+/* Eval-mode forward (running statistics, no dropout): one fused kernel.  model.py:161/220, ui.py:35. */
+int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const float* bn_buffers,
+                        const float* x, float* logits, void* stream);
+
+/* torch.optim.Adam step (weight_decay 0, amsgrad off) over n elements; `step` is a device int32
+ * that is incremented in-kernel (graph-capturable).  torch/optim/adam.py:457,476,531-547. */
+int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_avg,
+                     float* exp_avg_sq, int32_t* step, float lr, float beta1, float beta2,
+                     float eps, void* stream);
+
+/* One fused hot-loop iteration (model.py:141-148): forward_train + CE + backward + clamps + Adam.
+ * adam_state = [exp_avg | exp_avg_sq] (2 * param_count floats); step as in eegnet_adam_step. */
+int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers, const float* x,
+                      const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
+                      float* adam_state, int32_t* step, float lr, float beta1, float beta2,
+                      float eps, float* loss, float* logits, void* ws, void* stream);
+
+/* Thread-local description of the last error ("" if none). */
+const char* eegnet_last_error(void);
+
+/* Library/build identification string (gfx target, build flags). */
+const char* eegnet_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EEGNET_ABI_H */

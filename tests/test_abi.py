@@ -1,0 +1,56 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports every symbol that
+include/eegnet_abi.h declares; host-side geometry/validation calls work without a GPU."""
+
+from __future__ import annotations
+
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "eegnet_abi.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(eegnet_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_matches_binding():
+    from eegnetreplication_amd import _lib
+    assert _header_symbols() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    from eegnetreplication_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libeegnet_hip.so not built (run __graft_entry__.build())")
+    lib = _lib.load()
+    for name in _header_symbols():
+        assert hasattr(lib, name), name
+    assert b"gfx950" in lib.eegnet_build_info()
+
+
+def test_param_count_and_validation():
+    from eegnetreplication_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libeegnet_hip.so not built")
+    d = _lib.dims(4096, 22, 256)
+    assert _lib.param_count(d) == 1716          # paper Table 3 / SURVEY section 6
+    assert _lib.workspace_bytes(d) > 4 * 4096 * 16 * 64 * 4
+    d16 = _lib.dims(8, 64, 512, F1=16, D=4)
+    assert _lib.param_count(d16) == 14116       # EEGNet-16,4 at 64x512
+    with pytest.raises(RuntimeError, match="K1"):
+        _lib.param_count(_lib.dims(8, 22, 256, K1=48))
+    with pytest.raises(RuntimeError, match="F1\\*D"):
+        _lib.param_count(_lib.dims(8, 22, 256, F1=3, D=1))
+
+
+def test_shape_param_layout_matches_library():
+    from eegnetreplication_amd import _lib
+    from eegnetreplication_amd.ops import Shape
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libeegnet_hip.so not built")
+    for C, T, F1, D in [(22, 256, 8, 2), (22, 257, 8, 2), (64, 512, 16, 4), (8, 64, 8, 2)]:
+        s = Shape(C=C, T=T, F1=F1, D=D)
+        assert s.n_params() == _lib.param_count(s.dims(4))

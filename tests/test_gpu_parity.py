@@ -1,0 +1,169 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference golden vectors and the CPU
+oracle on identical weights, inputs and dropout masks.  Tolerance (north_star): fp32 logits and
+gradients within rtol 1e-4 (atol 1e-5 * max|ref|), see tests/golden_util.py."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import (Golden, PARAM_NAMES, assert_close, assert_grads_close,
+                         assert_params_close, fixture_names, make_inputs, make_masks)
+
+pytestmark = pytest.mark.gpu
+
+TRAIN_FIXTURES = [n for n in fixture_names() if n not in ("G3",)]
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _model_from(g: Golden, dev):
+    from eegnetreplication_amd import EEGNet
+    m = g.meta
+    model = EEGNet(m["C"], m["T"], F1=m["F1"], D=m["D"], p=m["p"])
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in g.init.items()})
+    return model.to(dev)
+
+
+@pytest.mark.parametrize("name", TRAIN_FIXTURES)
+def test_train_step_matches_reference(name):
+    dev = _dev()
+    g = Golden(name)
+    m = g.meta
+    model = _model_from(g, dev).train()
+    masks = g.masks(0)
+    if masks is not None:
+        model.set_dropout_masks(torch.from_numpy(masks[0]).to(dev), torch.from_numpy(masks[1]).to(dev))
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, eps=1e-7)
+    x = torch.from_numpy(g.x).to(dev)
+    y = torch.from_numpy(g.y).to(dev)
+    logits = model(x)
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    opt.zero_grad()
+    (loss * m["loss_scale"]).backward()
+    assert_close(logits.detach().cpu().numpy(), g.z["logits"], name="logits")
+    assert abs(float(loss) - float(g.z["loss"])) <= 1e-4 * max(1.0, abs(float(g.z["loss"])))
+    assert_grads_close({k: p.grad.cpu().numpy() for k, p in model.named_parameters()},
+                       g.group("grad"), prefix="grad.")
+    bufs = {k: b.cpu().numpy() for k, b in model.named_buffers()}
+    for k, v in g.group("buf1").items():
+        assert_close(bufs[k], v, name=k)
+    opt.step()
+    assert_params_close({k: p.detach().cpu().numpy() for k, p in model.named_parameters()},
+                        g.group("step1"), prefix="step1.")
+
+
+def test_eval_logits_match_reference():
+    dev = _dev()
+    g = Golden("G3")
+    model = _model_from(g, dev).eval()
+    with torch.no_grad():
+        out = model(torch.from_numpy(g.x).to(dev))
+    assert_close(out.cpu().numpy(), g.z["eval_logits"], name="eval_logits")
+
+
+@pytest.mark.parametrize("name", ["G1", "G5_B1", "G5_8x64"])
+def test_fused_train_step_matches_reference(name):
+    """eegnet_train_step (forward + CE + backward + clamps + Adam in one device sequence)."""
+    from eegnetreplication_amd import FusedTrainer
+    dev = _dev()
+    g = Golden(name)
+    if g.meta["p"] != 0:
+        pytest.skip("fused path draws masks on device")
+    model = _model_from(g, dev).train()
+    tr = FusedTrainer(model, lr=1e-3, eps=1e-7)
+    x = torch.from_numpy(g.x).to(dev)
+    y = torch.from_numpy(g.y).to(dev)
+    logits = torch.empty((x.shape[0], 4), device=dev)
+    loss = tr.step(x, y, logits=logits)
+    assert_close(logits.cpu().numpy(), g.z["logits"], name="logits")
+    assert abs(float(loss) - float(g.z["loss"])) <= 1e-4 * max(1.0, abs(float(g.z["loss"])))
+    from eegnetreplication_amd.ops import Shape  # noqa: F401
+    n = 0
+    gr = {}
+    for k, p in model.named_parameters():
+        gr[k] = tr.adam.grads[n:n + p.numel()].view(p.shape).cpu().numpy()
+        n += p.numel()
+    assert_grads_close(gr, g.group("grad"), prefix="grad.")
+    assert_params_close({k: p.detach().cpu().numpy() for k, p in model.named_parameters()},
+                        g.group("step1"), prefix="step1.")
+
+
+def test_fused_trajectory_G7():
+    """20 fused steps on one batch (p=0) follow the reference loss trajectory."""
+    from eegnetreplication_amd import FusedTrainer
+    dev = _dev()
+    g = Golden("G7")
+    model = _model_from(g, dev).train()
+    tr = FusedTrainer(model, lr=1e-3, eps=1e-7)
+    x = torch.from_numpy(g.x).to(dev)
+    y = torch.from_numpy(g.y).to(dev)
+    losses = []
+    for _ in range(g.meta["steps"]):
+        losses.append(float(tr.step(x, y)))
+    np.testing.assert_allclose(losses, g.z["losses"], rtol=2e-4)
+    assert_params_close({k: p.detach().cpu().numpy() for k, p in model.named_parameters()},
+                        g.group("final"), steps=g.meta["steps"], rtol=2e-4, atol_frac=2e-4)
+
+
+def test_large_batch_against_torch_fp32():
+    """cfg2 shape (B=4096, 22x256, p=0.5): HIP grads vs the torch fp32 restatement on the same
+    device with the same injected masks (size-independent check at the benchmark size)."""
+    from eegnetreplication_amd import EEGNet
+    from oracle import torch_ref as tr
+    dev = _dev()
+    B, C, T = 4096, 22, 256
+    torch.manual_seed(0)
+    model = EEGNet(C, T, p=0.5).to(dev).train()
+    state = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    x_np, y_np = make_inputs(B, C, T, 1234)
+    m2, m3 = make_masks(B, 16, T, 99, 0.5)
+    x, y = torch.from_numpy(x_np).to(dev), torch.from_numpy(y_np).to(dev)
+    model.set_dropout_masks(torch.from_numpy(m2).to(dev), torch.from_numpy(m3).to(dev))
+    logits = model(x)
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    ref = tr.TorchRefEEGNet(state, p=0.5, device=dev)
+    rl = ref(x, (torch.from_numpy(m2).to(dev), torch.from_numpy(m3).to(dev)))
+    rloss = torch.nn.functional.cross_entropy(rl, y)
+    rloss.backward()
+    assert_close(logits.detach().cpu().numpy(), rl.detach().cpu().numpy(), name="logits")
+    assert_grads_close({k: p.grad.cpu().numpy() for k, p in model.named_parameters()},
+                       {k: ref.params[k].grad.cpu().numpy() for k in PARAM_NAMES},
+                       rtol=1e-3, atol_frac=1e-4, prefix="B4096 grad.")
+    for k, b in model.named_buffers():
+        if "running" in k:
+            assert_close(b.cpu().numpy(), ref.buffers[k].cpu().numpy(), name=k)
+
+
+def test_dropout_generator_properties():
+    """On-device masks: deterministic per (seed, offset), keep rate 1-p, forward/backward agree."""
+    from eegnetreplication_amd import EEGNet
+    from eegnetreplication_amd import ops
+    dev = _dev()
+    B, C, T = 512, 22, 256
+    torch.manual_seed(3)
+    model = EEGNet(C, T, p=0.5).to(dev).train()
+    x_np, y_np = make_inputs(B, C, T, 5)
+    x = torch.from_numpy(x_np).to(dev)
+    shape = model.shape
+    ws = ops.new_workspace(shape, B, dev)
+    flat = model.flat_parameters().clone()
+    bn = model.flat_bn_buffers().clone()
+    l1 = ops.forward_train(shape, flat, bn.clone(), x, ws, 11, 1)
+    l2 = ops.forward_train(shape, flat, bn.clone(), x, ws, 11, 1)
+    l3 = ops.forward_train(shape, flat, bn.clone(), x, ws, 11, 2)
+    assert torch.equal(l1, l2)
+    assert not torch.equal(l1, l3)
+    # the injected-mask path and the generator path share the same kernels: with p = 0 both are
+    # the identity and must agree bit for bit
+    from eegnetreplication_amd.ops import Shape
+    s0 = Shape(**{**shape.__dict__, "p": 0.0})
+    a = ops.forward_train(s0, flat, bn.clone(), x, ws, 11, 1)
+    b = ops.forward_train(s0, flat, bn.clone(), x, ws, 12, 7)
+    assert torch.equal(a, b)
