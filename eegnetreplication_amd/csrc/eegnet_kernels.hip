@@ -842,7 +842,7 @@ __global__ __launch_bounds__(NT) void k_pass_e(Geo g, const float* __restrict__ 
     }
     __syncthreads();
     // Xm: waves hold (tile, ksplit) accumulators -> LDS [ksplit][FO][16*NCT] -> sum over ksplit
-    float* XR = Xs;      // reuse
+    float* XR = Xs;      // reuse the x / s / dy rows (contiguous, (C + 2 F2) * RS floats)
     const int XW = 16 * g.NCT;
 #pragma unroll
     for (int ui = 0; ui < MAXU; ++ui) {
@@ -1294,7 +1294,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
               g->F2 * g->F2 + 18 * g->F2;
     {
         const int xr = 4 * g->FO * 16 * g->NCT;    // Xm reduction scratch (reuses Xs)
-        if (launch && xr > g->C * g->RS) return fail(EEGNET_EINVAL, "internal: Xm scratch does not fit");
+        if (launch && xr > (g->C + 2 * g->F2) * g->RS)
+            return fail(EEGNET_EINVAL, "internal: Xm scratch does not fit");
     }
     g->ldsE = rows + g->F2 * g->RS + rup(g->F2 * g->T1, 4) + wsh + 2 * NT;
     g->ldsI = rows + b2 + wsh + rup(g->NF, 4) + 4 * g->F2;
