@@ -1,0 +1,230 @@
+"""Benchmark: EEGNet-8,2 train step (forward + CE + backward + clamps + Adam) on synthetic
+22ch x 256 trials, batch 4096 per GPU, fp32, HIP kernels (BASELINE.json configs[1] / cfg4).
+
+    python bench.py [--gpus N --steps K --warmup W]            (N=1)
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints ONE JSON line on rank 0.  `value` = trials/s over all ranks (weak scaling: 4096 trials per
+GPU per step; N>1 = data parallel with one RCCL gradient all-reduce per step).  `roofline` is for the
+kernel with the largest device time, from HIP events recorded inside the timed region;
+`cpu_baseline` times the stock-PyTorch CPU restatement of the reference step (oracle/torch_ref.py)
+on this host's cores over a bounded sample.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3      # MI355X FP32 dense (vector == matrix on gfx950), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0         # MI355X HBM3E spec
+REF_FLOP_PER_TRIAL = 6_507_520   # reference formulation, fwd+bwd conv/linear MACx2
+ALG_BYTES_PER_TRIAL = 45_056     # x read twice
+
+
+def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
+    """Per-trial algorithmic FLOPs (MAC x 2) and HBM bytes of each pass kernel as implemented
+    (DESIGN.md section 4).  Returns {kernel: (flop, bytes)}."""
+    F2 = F1 * D
+    T1, T2 = T // 4, T // 128
+    npairs = K1 * (K1 - 1) // 2
+    sp = F2 * C * T                  # spatial GEMM
+    fir = F2 * T * K1                # one 32-tap FIR over the F2 rows
+    b2 = F2 * T1 * 16 + F2 * F2 * T1  # block_2 forward (dw16 + pw)
+    xb = C * T * 4
+    row = F2 * T1 * 4
+    return {
+        "k_pass_a": (2 * (sp + fir + C * T * K1 + 2 * C * npairs), xb),
+        "k_pass_b": (2 * (sp + fir + b2), xb + 3 * row),
+        "k_pass_c": (2 * (b2 + 2 * 4 * F2 * T2), row + 16),
+        "k_pass_d": (2 * (b2 + 2 * F2 * F2 * T1 + 2 * F2 * T1 * 16), 4 * row + 16),
+        "k_pass_e": (2 * (sp + 3 * fir + sp), xb + row),
+    }
+
+
+def cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(B, C, T, steps, threads):
+    """Reference CPU path (stock ATen via oracle/torch_ref.py) on this host; trials/s."""
+    from oracle import torch_ref as tr
+    from eegnetreplication_amd import EEGNet
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    state = {k: v.numpy() for k, v in EEGNet(C, T, p=0.5).state_dict().items()}
+    ref = tr.TorchRefEEGNet(state, p=0.5)
+    opt = tr.make_optimizer(ref)
+    rng = np.random.default_rng(1234)
+    x = torch.from_numpy(rng.standard_normal((B, C, T), dtype=np.float32))
+    y = torch.from_numpy(np.random.default_rng(1235).integers(0, 4, B))
+    tr.train_step(ref, opt, x, y)            # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.train_step(ref, opt, x, y)
+    dt = time.perf_counter() - t0
+    return B * steps / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4096, help="trials per GPU per step")
+    ap.add_argument("--C", type=int, default=22)
+    ap.add_argument("--T", type=int, default=256)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
+    from eegnetreplication_amd.distributed import DataParallelTrainer, init_process_group
+
+    rank, world, local = init_process_group()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B, C, T = args.batch, args.C, args.T
+
+    torch.manual_seed(0)
+    model = EEGNet(C, T, F1=8, D=2, p=0.5).to(dev).train()
+    rng = np.random.default_rng(1234 + rank)
+    x = torch.from_numpy(rng.standard_normal((B, C, T), dtype=np.float32)).to(dev)
+    y = torch.from_numpy(np.random.default_rng(1235 + rank).integers(0, 4, B)).to(dev)
+    trainer = DataParallelTrainer(model) if world > 1 else FusedTrainer(model)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    prof = not args.no_profile
+    for _ in range(args.warmup):
+        trainer.step(x, y)
+    if prof:                       # fill the library's event pool outside the timed region
+        _lib.profile_enable(True)
+        trainer.step(x, y)
+        torch.cuda.synchronize()
+        _lib.profile_collect()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step(x, y)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern = _lib.profile_collect() if prof else {}
+    if prof:
+        _lib.profile_enable(False)
+    loss = float(trainer.loss.item())
+
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ms_per_step = 1e3 * dt / args.steps
+    trials_per_s = world * B * args.steps / dt
+
+    if rank == 0:
+        alg = kernel_algorithmic(C, T)
+        per_kernel = {}
+        for name, (cnt, tot) in kern.items():
+            avg_ms = tot / max(cnt, 1)
+            e = {"launches": cnt, "avg_us": round(1e3 * avg_ms, 2),
+                 "share": round(tot / max(sum(v[1] for v in kern.values()), 1e-12), 4)}
+            if name in alg:
+                fl, by = alg[name]
+                e["alg_tflops"] = round(fl * B / (avg_ms * 1e-3) / 1e12, 2)
+                e["alg_gbs"] = round(by * B / (avg_ms * 1e-3) / 1e9, 1)
+            per_kernel[name] = e
+        roof = None
+        cand = {k: v for k, v in kern.items() if k in alg}
+        if cand:
+            dom = max(cand, key=lambda k: cand[k][1])
+            cnt, tot = cand[dom]
+            avg_s = tot / cnt * 1e-3
+            fl, by = alg[dom]
+            intensity = fl / by
+            ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+            pmc = {}
+            pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc_path):
+                with open(pmc_path) as f:
+                    pmc = json.load(f)
+            traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc else None
+            if intensity >= ridge:
+                ach = fl * B / avg_s / 1e12
+                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+                        "traffic": traffic, "kernel": dom, "avg_us": round(avg_s * 1e6, 2),
+                        "alg_flop_per_launch": fl * B, "alg_bytes_per_launch": by * B,
+                        "note": "fp32 VALU + f32 MFMA share the 157.3 TFLOP/s FP32 peak on gfx950"}
+            else:
+                ach = by * B / avg_s / 1e9
+                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                        "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic,
+                        "kernel": dom, "avg_us": round(avg_s * 1e6, 2),
+                        "alg_bytes_per_launch": by * B}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            threads = min(16, len(os.sched_getaffinity(0)))
+            v, secs = cpu_baseline(B, C, T, args.cpu_steps, threads)
+            cpu = {"value": round(v, 1), "unit": "trials/s", "cores": threads, "kind": "port",
+                   "sample": f"{args.cpu_steps} train steps (fwd+CE+bwd+Adam) of B={B} x {C}x{T} "
+                             f"after 1 warm-up, {secs:.1f} s, torch {torch.__version__} CPU, "
+                             f"{cpu_model_name()}"}
+        out = {
+            "metric": "train trials/sec (fwd+bwd) EEGNet-8,2 22ch x 256",
+            "value": round(trials_per_s, 1),
+            "unit": "trials/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (N(0,1) x, uniform labels; random-init EEGNet-8,2)",
+            "config": {"workload": f"EEGNet-8,2 train step (fwd+CE+bwd+clamps+Adam), {C}ch x {T}, "
+                                   f"batch {B}/GPU, p=0.5, fp32 HIP kernels",
+                       "model": "EEGNet-8,2", "global_batch": B * world, "seq_len": T,
+                       "channels": C, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "hbm_fraction": round(ALG_BYTES_PER_TRIAL * trials_per_s / (PEAK_HBM_GBS * 1e9), 4),
+            "ref_formulation_tflops": round(REF_FLOP_PER_TRIAL * trials_per_s / 1e12, 2),
+            "kernels": per_kernel,
+            "final_loss": round(loss, 5),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

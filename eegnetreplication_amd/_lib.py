@@ -33,14 +33,18 @@ _SIGS = {
     "eegnet_forward_train": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp,
                                             ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp]),
     "eegnet_backward": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp, _vp,
-                                       ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
+                                       ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp,
+                                       ctypes.c_int]),
+    "eegnet_clamp_grads": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp]),
     "eegnet_forward_eval": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp]),
     "eegnet_adam_step": (ctypes.c_int, [ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_float,
                                         ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp]),
     "eegnet_train_step": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, ctypes.c_uint64,
                                          ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
-                                         _vp, _vp]),
+                                         _vp, _vp, ctypes.c_int]),
+    "eegnet_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "eegnet_profile_collect": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp, ctypes.c_int, _vp]),
     "eegnet_last_error": (ctypes.c_char_p, []),
     "eegnet_build_info": (ctypes.c_char_p, []),
 }
@@ -91,3 +95,25 @@ def workspace_bytes(d: Dims) -> int:
     check(load().eegnet_workspace_bytes(ctypes.byref(d), ctypes.byref(out)),
           "eegnet_workspace_bytes")
     return int(out.value)
+
+
+def profile_enable(on: bool = True):
+    check(load().eegnet_profile_enable(1 if on else 0), "eegnet_profile_enable")
+
+
+def profile_collect() -> dict:
+    """{kernel name: (launches, total device ms)} since the last collect."""
+    cap = 32
+    names = ctypes.create_string_buffer(32 * cap)
+    counts = (ctypes.c_int * cap)()
+    tot = (ctypes.c_double * cap)()
+    n = ctypes.c_int(0)
+    check(load().eegnet_profile_collect(names, ctypes.cast(counts, ctypes.c_void_p),
+                                        ctypes.cast(tot, ctypes.c_void_p), cap,
+                                        ctypes.cast(ctypes.pointer(n), ctypes.c_void_p)),
+          "eegnet_profile_collect")
+    out = {}
+    for i in range(n.value):
+        nm = names.raw[32 * i:32 * i + 32].split(b"\0", 1)[0].decode()
+        out[nm] = (int(counts[i]), float(tot[i]))
+    return out

@@ -30,6 +30,7 @@
 #include <math.h>
 #include <string>
 #include <algorithm>
+#include <vector>
 #include <stdarg.h>
 
 #include "../../include/eegnet_abi.h"
@@ -57,6 +58,7 @@ struct Geo {
     int npairs;          // lag-Gram edge pairs K1*(K1-1)/2
     float p, scale, eps, mom;
     int drop;
+    int noclamp;          // skip the model.py:44/84 clamps (data-parallel: clamp after all-reduce)
     unsigned long long key;
     // flat parameter offsets (named_parameters order)
     int o_w1, o_g1, o_b1, o_ws, o_g2, o_b2, o_w2, o_W3, o_g3, o_b3, o_Wfc, o_bfc, nparam;
@@ -221,7 +223,7 @@ __device__ __forceinline__ void load_block2_weights(const Geo& g, const float* _
 // part row: [G0 K1][S0][Ed npairs][e1 K1-1][Sv F2][Sv2 F2]
 // ================================================================================================
 template <int K1>
-__global__ __launch_bounds__(NT) void k_pass_a(Geo g, const float* __restrict__ prm,
+__global__ __launch_bounds__(NT, 2) void k_pass_a(Geo g, const float* __restrict__ prm,
                                                const float* __restrict__ x, float* __restrict__ part) {
     using G_ = KG<K1>;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(NT) void k_pass_a(Geo g, const float* __restrict__ 
 // part row: [Sr F2][Sr2 F2]
 // ================================================================================================
 template <int K1>
-__global__ __launch_bounds__(NT) void k_pass_b(Geo g, const float* __restrict__ prm,
+__global__ __launch_bounds__(NT, 2) void k_pass_b(Geo g, const float* __restrict__ prm,
                                                const float* __restrict__ coef,
                                                const float* __restrict__ x,
                                                const uint8_t* __restrict__ mask2,
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(NT) void k_pass_d(Geo g, const float* __restrict__ 
 // part row: [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2]
 // ================================================================================================
 template <int K1>
-__global__ __launch_bounds__(NT) void k_pass_e(Geo g, const float* __restrict__ prm,
+__global__ __launch_bounds__(NT, 2) void k_pass_e(Geo g, const float* __restrict__ prm,
                                                const float* __restrict__ coef,
                                                const float* __restrict__ x,
                                                const float* __restrict__ dp2g,
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(NT) void k_pass_e(Geo g, const float* __restrict__ 
 // Eval-mode forward: one fused kernel per trial (BN running statistics folded; no dropout).
 // ================================================================================================
 template <int K1>
-__global__ __launch_bounds__(NT) void k_infer(Geo g, const float* __restrict__ prm,
+__global__ __launch_bounds__(NT, 2) void k_infer(Geo g, const float* __restrict__ prm,
                                               const float* __restrict__ bn,
                                               const float* __restrict__ x, float* __restrict__ logits) {
     using G_ = KG<K1>;
@@ -962,18 +964,35 @@ __global__ __launch_bounds__(NT) void k_infer(Geo g, const float* __restrict__ p
 }
 
 // ================================================================================================
-// Deterministic fp64 column reduction of per-workgroup partial rows.
+// Deterministic fp64 column reduction of per-workgroup partial rows, stage 1: the rows are cut into
+// RCH chunks; workgroup (column block, chunk) writes one fp64 partial per column.  Stage 2 (the
+// RCH-way sum per column) is the prologue of the finalize kernel that consumes the sums.
 // ================================================================================================
+constexpr int RCH = 32;
+
 __global__ __launch_bounds__(NT) void k_colsum(const float* __restrict__ part, int nrows, int ncols,
-                                               double* __restrict__ out) {
+                                               double* __restrict__ part2) {
     __shared__ double red[4][64];
     const int tid = threadIdx.x, col = blockIdx.x * 64 + (tid & 63), rg = tid >> 6;
+    const int r0 = (nrows * (int)blockIdx.y) / RCH, r1 = (nrows * ((int)blockIdx.y + 1)) / RCH;
     double a = 0.0;
     if (col < ncols)
-        for (int r = rg; r < nrows; r += 4) a += (double)part[(size_t)r * ncols + col];
+        for (int r = r0 + rg; r < r1; r += 4) a += (double)part[(size_t)r * ncols + col];
     red[rg][tid & 63] = a;
     __syncthreads();
-    if (tid < 64 && col < ncols) out[col] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    if (tid < 64 && col < ncols)
+        part2[(size_t)blockIdx.y * ncols + col] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
+// stage 2, run by the one finalize workgroup: S[c] = sum over the RCH chunk partials
+__device__ __forceinline__ void reduce_chunks(const double* __restrict__ part2, int ncols, double* S) {
+    for (int c = threadIdx.x; c < ncols; c += NT) {
+        double a = 0.0;
+#pragma unroll 8
+        for (int r = 0; r < RCH; ++r) a += part2[(size_t)r * ncols + c];
+        S[c] = a;
+    }
+    __syncthreads();
 }
 
 // ================================================================================================
@@ -987,7 +1006,7 @@ __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, doub
 
 // after pass A: BN1 (model.py:32) and BN2 (model.py:47) batch statistics
 __global__ __launch_bounds__(NT) void k_fin1(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ sums,
+                                             const double* __restrict__ part2,
                                              double* __restrict__ stats, float* __restrict__ coef,
                                              float* __restrict__ bn, int update_running) {
     extern __shared__ __attribute__((aligned(16))) double dsm[];
@@ -996,7 +1015,9 @@ __global__ __launch_bounds__(NT) void k_fin1(Geo g, const float* __restrict__ pr
     double* S1 = Gm + K1 * K1;        // K1
     double* a1s = S1 + K1;            // F1
     double* c1s = a1s + 64;
+    double* sums = c1s + 64;          // nA
     const int tid = threadIdx.x;
+    reduce_chunks(part2, g.nA, sums);
     const double* G0 = sums;
     const double S0 = sums[K1];
     const double* Ed = sums + K1 + 1;
@@ -1064,9 +1085,11 @@ __global__ __launch_bounds__(NT) void k_fin1(Geo g, const float* __restrict__ pr
 }
 
 // after pass B: BN3 (model.py:71) batch statistics
-__global__ __launch_bounds__(NT) void k_fin2(Geo g, const double* __restrict__ sums,
+__global__ __launch_bounds__(NT) void k_fin2(Geo g, const double* __restrict__ part2,
                                              float* __restrict__ coef, float* __restrict__ bn,
                                              int update_running) {
+    extern __shared__ __attribute__((aligned(16))) double sums[];
+    reduce_chunks(part2, g.nB, sums);
     const int j = threadIdx.x;
     if (j >= g.F2) return;
     const double n3 = (double)g.B * g.T1;
@@ -1080,12 +1103,17 @@ __global__ __launch_bounds__(NT) void k_fin2(Geo g, const double* __restrict__ s
 
 // after pass C: classifier grads (+ clamp, model.py:84), BN3 grads and backward constants
 __global__ __launch_bounds__(NT) void k_fin3(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ sums,
+                                             const double* __restrict__ part2,
                                              float* __restrict__ coef, float* __restrict__ grads,
                                              float* __restrict__ loss, int ce) {
+    extern __shared__ __attribute__((aligned(16))) double sums[];
+    reduce_chunks(part2, g.nC, sums);
     const int tid = threadIdx.x;
     const int n4 = NCLS * g.NF;
-    for (int p = tid; p < n4; p += NT) grads[g.o_Wfc + p] = fminf(fmaxf((float)sums[p], -0.25f), 0.25f);
+    for (int p = tid; p < n4; p += NT) {
+        const float v = (float)sums[p];
+        grads[g.o_Wfc + p] = g.noclamp ? v : fminf(fmaxf(v, -0.25f), 0.25f);
+    }
     if (tid < NCLS) grads[g.o_bfc + tid] = (float)sums[n4 + tid];
     if (tid < g.F2) {
         const int j = tid;
@@ -1107,8 +1135,10 @@ __global__ __launch_bounds__(NT) void k_fin3(Geo g, const float* __restrict__ pr
 
 // after pass D: block_2 grads, BN2 grads and the dy2 constants
 __global__ __launch_bounds__(NT) void k_fin4(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ sums,
+                                             const double* __restrict__ part2,
                                              float* __restrict__ coef, float* __restrict__ grads) {
+    extern __shared__ __attribute__((aligned(16))) double sums[];
+    reduce_chunks(part2, g.nD, sums);
     const int tid = threadIdx.x;
     for (int p = tid; p < g.F2 * g.F2; p += NT) grads[g.o_W3 + p] = (float)sums[p];
     for (int p = tid; p < g.F2 * 16; p += NT) grads[g.o_w2 + p] = (float)sums[g.F2 * g.F2 + p];
@@ -1128,10 +1158,12 @@ __global__ __launch_bounds__(NT) void k_fin4(Geo g, const float* __restrict__ pr
 
 // after pass E: spatial grad (+ clamp, model.py:44), BN1 grads, temporal-conv grad
 __global__ __launch_bounds__(NT) void k_fin5(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ sums,
+                                             const double* __restrict__ part2,
                                              const double* __restrict__ stats,
                                              const float* __restrict__ coef,
                                              float* __restrict__ grads) {
+    extern __shared__ __attribute__((aligned(16))) double sums[];
+    reduce_chunks(part2, g.nE, sums);
     __shared__ double db1s[64], dg1s[64];
     const int tid = threadIdx.x, K1 = g.K1;
     const double* Q = sums;
@@ -1143,7 +1175,7 @@ __global__ __launch_bounds__(NT) void k_fin5(Geo g, const float* __restrict__ pr
     for (int p = tid; p < g.F2 * g.C; p += NT) {
         const int o = p / g.C, gg = o / g.D;
         const double v = (double)coef[CF_A1 * CSTR + gg] * Xm[p] + (double)coef[CF_C1 * CSTR + gg] * Sdy[o];
-        grads[g.o_ws + p] = fminf(fmaxf((float)v, -1.0f), 1.0f);
+        grads[g.o_ws + p] = g.noclamp ? (float)v : fminf(fmaxf((float)v, -1.0f), 1.0f);
     }
     const double n1 = (double)g.B * g.C * g.T;
     if (tid < g.F1) {
@@ -1197,6 +1229,13 @@ __global__ __launch_bounds__(NT) void k_adam(int64_t n, float* __restrict__ p, c
 }
 
 __global__ void k_step_inc(int32_t* step) { if (threadIdx.x == 0) *step += 1; }
+
+// the two gradient hooks of model.py:44 and model.py:84, applied to a flat grad buffer
+__global__ __launch_bounds__(NT) void k_clamp(Geo g, float* __restrict__ grads) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i < g.F2 * g.C) grads[g.o_ws + i] = fminf(fmaxf(grads[g.o_ws + i], -1.0f), 1.0f);
+    if (i < NCLS * g.NF) grads[g.o_Wfc + i] = fminf(fmaxf(grads[g.o_Wfc + i], -0.25f), 0.25f);
+}
 
 }  // namespace eeg
 
@@ -1315,7 +1354,7 @@ static WsLayout make_layout(const Geo& g) {
     L.partD = take((size_t)g.gD * g.nD * 4);
     L.partE = take((size_t)g.gE * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
-    L.sums = take((size_t)nmax * 8);
+    L.sums = take((size_t)nmax * 8 * RCH);
     L.stats = take((size_t)(g.K1 * g.K1 + g.K1) * 8);
     L.coef = take((size_t)CF_COUNT * CSTR * 4);
     const size_t per = (size_t)g.B * g.F2 * g.T1 * 4;
@@ -1331,6 +1370,31 @@ static uint64_t mix_key(uint64_t seed, uint64_t offset) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+
+// ---- optional per-kernel device timing (bench / roofline), off by default ----
+enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_COLSUM, KID_FIN, KID_ADAM, KID_INFER, KID_COUNT };
+static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
+                                              "k_colsum", "k_fin", "k_adam", "k_infer"};
+struct ProfRec { int kid; hipEvent_t a, b; };
+struct ProfState { bool on = false; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
+static thread_local ProfState g_prof;
+
+static hipEvent_t prof_event() {
+    if (!g_prof.pool.empty()) { hipEvent_t e = g_prof.pool.back(); g_prof.pool.pop_back(); return e; }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+struct ProfScope {
+    int kid; hipStream_t s; hipEvent_t a = nullptr;
+    ProfScope(int k, hipStream_t st) : kid(k), s(st) {
+        if (g_prof.on) { a = prof_event(); hipEventRecord(a, s); }
+    }
+    ~ProfScope() {
+        if (a) { hipEvent_t b = prof_event(); hipEventRecord(b, s); g_prof.recs.push_back({kid, a, b}); }
+    }
+};
+#define PROF(kid) ProfScope prof_scope_##kid(kid, s)
 
 #define LAUNCH_CHECK(what)                                                            \
     do {                                                                              \
@@ -1359,7 +1423,8 @@ static void ensure_attrs() {
 }
 
 static int colsum(const float* part, int nrows, int ncols, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_colsum, dim3((ncols + 63) / 64), dim3(NT), 0, s, part, nrows, ncols, out);
+    PROF(KID_COLSUM);
+    hipLaunchKernelGGL(k_colsum, dim3((ncols + 63) / 64, RCH), dim3(NT), 0, s, part, nrows, ncols, out);
     LAUNCH_CHECK("k_colsum");
     return 0;
 }
@@ -1370,18 +1435,18 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
                        int c_mode, const int64_t* labels, float* loss, float* grads, hipStream_t s) {
     double* sums = (double*)(ws + L.sums);
     float* coef = (float*)(ws + L.coef);
-    hipLaunchKernelGGL(k_pass_a<K1>, dim3(g.gA), dim3(NT), g.ldsA * 4, s, g, params, x, (float*)(ws + L.partA));
-    LAUNCH_CHECK("k_pass_a");
+    { PROF(KID_A); hipLaunchKernelGGL(k_pass_a<K1>, dim3(g.gA), dim3(NT), g.ldsA * 4, s, g, params, x, (float*)(ws + L.partA));
+    } LAUNCH_CHECK("k_pass_a");
     if (int r = colsum((float*)(ws + L.partA), g.gA, g.nA, sums, s)) return r;
-    hipLaunchKernelGGL(k_fin1, dim3(1), dim3(NT), (g.K1 * g.K1 + g.K1 + 128) * 8, s, g, params, sums,
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin1, dim3(1), dim3(NT), (g.K1 * g.K1 + g.K1 + 128 + g.nA) * 8, s, g, params, sums,
                        (double*)(ws + L.stats), coef, bn, update_running);
-    LAUNCH_CHECK("k_fin1");
-    hipLaunchKernelGGL(k_pass_b<K1>, dim3(g.gB), dim3(NT), g.ldsB * 4, s, g, params, coef, x, m2,
+    } LAUNCH_CHECK("k_fin1");
+    { PROF(KID_B); hipLaunchKernelGGL(k_pass_b<K1>, dim3(g.gB), dim3(NT), g.ldsB * 4, s, g, params, coef, x, m2,
                        (float*)(ws + L.d2), (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.partB));
-    LAUNCH_CHECK("k_pass_b");
+    } LAUNCH_CHECK("k_pass_b");
     if (int r = colsum((float*)(ws + L.partB), g.gB, g.nB, sums, s)) return r;
-    hipLaunchKernelGGL(k_fin2, dim3(1), dim3(NT), 0, s, g, sums, coef, bn, update_running);
-    LAUNCH_CHECK("k_fin2");
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin2, dim3(1), dim3(NT), g.nB * 8, s, g, sums, coef, bn, update_running);
+    } LAUNCH_CHECK("k_fin2");
     (void)labels; (void)loss; (void)grads; (void)c_mode; (void)logits;
     return 0;
 }
@@ -1394,28 +1459,28 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, const float* 
     double* sums = (double*)(ws + L.sums);
     float* coef = (float*)(ws + L.coef);
     float* dl = dlogits ? (float*)dlogits : (float*)(ws + L.dl);
-    hipLaunchKernelGGL(k_pass_c, dim3(g.gC), dim3(NT), g.ldsC * 4, s, g, params, coef,
+    { PROF(KID_C); hipLaunchKernelGGL(k_pass_c, dim3(g.gC), dim3(NT), g.ldsC * 4, s, g, params, coef,
                        (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
                        (float*)(ws + L.partC), c_mode);
-    LAUNCH_CHECK("k_pass_c(bwd)");
+    } LAUNCH_CHECK("k_pass_c(bwd)");
     if (int r = colsum((float*)(ws + L.partC), g.gC, g.nC, sums, s)) return r;
-    hipLaunchKernelGGL(k_fin3, dim3(1), dim3(NT), 0, s, g, params, sums, coef, grads, loss,
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin3, dim3(1), dim3(NT), g.nC * 8, s, g, params, sums, coef, grads, loss,
                        (c_mode & PC_CE) ? 1 : 0);
-    LAUNCH_CHECK("k_fin3");
-    hipLaunchKernelGGL(k_pass_d, dim3(g.gD), dim3(NT), g.ldsD * 4, s, g, params, coef,
+    } LAUNCH_CHECK("k_fin3");
+    { PROF(KID_D); hipLaunchKernelGGL(k_pass_d, dim3(g.gD), dim3(NT), g.ldsD * 4, s, g, params, coef,
                        (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
                        m2, m3, (const float*)dl, (float*)(ws + L.dp2), (float*)(ws + L.partD));
-    LAUNCH_CHECK("k_pass_d");
+    } LAUNCH_CHECK("k_pass_d");
     if (int r = colsum((float*)(ws + L.partD), g.gD, g.nD, sums, s)) return r;
-    hipLaunchKernelGGL(k_fin4, dim3(1), dim3(NT), 0, s, g, params, sums, coef, grads);
-    LAUNCH_CHECK("k_fin4");
-    hipLaunchKernelGGL(k_pass_e<K1>, dim3(g.gE), dim3(NT), g.ldsE * 4, s, g, params, coef, x,
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin4, dim3(1), dim3(NT), g.nD * 8, s, g, params, sums, coef, grads);
+    } LAUNCH_CHECK("k_fin4");
+    { PROF(KID_E); hipLaunchKernelGGL(k_pass_e<K1>, dim3(g.gE), dim3(NT), g.ldsE * 4, s, g, params, coef, x,
                        (const float*)(ws + L.dp2), (float*)(ws + L.partE));
-    LAUNCH_CHECK("k_pass_e");
+    } LAUNCH_CHECK("k_pass_e");
     if (int r = colsum((float*)(ws + L.partE), g.gE, g.nE, sums, s)) return r;
-    hipLaunchKernelGGL(k_fin5, dim3(1), dim3(NT), 0, s, g, params, sums, (const double*)(ws + L.stats),
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin5, dim3(1), dim3(NT), g.nE * 8, s, g, params, sums, (const double*)(ws + L.stats),
                        (const float*)coef, grads);
-    LAUNCH_CHECK("k_fin5");
+    } LAUNCH_CHECK("k_fin5");
     return 0;
 }
 
@@ -1460,19 +1525,20 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, mask2, logits, 1, 0, nullptr, nullptr, nullptr, s)
                        : run_forward<64>(g, L, w, params, bn_buffers, x, mask2, logits, 1, 0, nullptr, nullptr, nullptr, s);
     if (r) return r;
-    hipLaunchKernelGGL(k_pass_c, dim3(g.gC), dim3(NT), g.ldsC * 4, s, g, params, (const float*)(w + L.coef),
+    { PROF(KID_C); hipLaunchKernelGGL(k_pass_c, dim3(g.gC), dim3(NT), g.ldsC * 4, s, g, params, (const float*)(w + L.coef),
                        (const float*)(w + L.d2), mask3, (const float*)nullptr, (const int64_t*)nullptr,
                        logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS);
-    LAUNCH_CHECK("k_pass_c(fwd)");
+    } LAUNCH_CHECK("k_pass_c(fwd)");
     return 0;
 }
 
 int eegnet_backward(const eegnet_dims* dims, const float* params, const float* x,
                     const float* dlogits, const int64_t* labels, const uint8_t* mask2,
                     const uint8_t* mask3, uint64_t seed, uint64_t offset, float* grads, float* loss,
-                    void* ws, void* stream) {
+                    void* ws, void* stream, int flags) {
     Geo g;
     if (int r = make_geo(dims, &g)) return r;
+    g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
     if (int r = check_ptrs(params, "params", x, "x")) return r;
     if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
     if (!dlogits && !labels) return fail(EEGNET_EINVAL, "need dlogits or labels");
@@ -1496,6 +1562,7 @@ int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const floa
     ensure_attrs();
     hipStream_t s = (hipStream_t)stream;
     const int grid = std::min(g.B, 1024);
+    PROF(KID_INFER);
     if (g.K1 == 32)
         hipLaunchKernelGGL(k_infer<32>, dim3(grid), dim3(NT), g.ldsI * 4, s, g, params, bn_buffers, x, logits);
     else
@@ -1510,9 +1577,9 @@ int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_av
     if (n <= 0) return fail(EEGNET_EINVAL, "n must be > 0");
     if (!params || !grads || !exp_avg || !exp_avg_sq || !step) return fail(EEGNET_EINVAL, "null pointer");
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, n, params, grads,
+    { PROF(KID_ADAM); hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, n, params, grads,
                        exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps);
-    LAUNCH_CHECK("k_adam");
+    } LAUNCH_CHECK("k_adam");
     hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(64), 0, s, step);
     LAUNCH_CHECK("k_step_inc");
     return 0;
@@ -1521,13 +1588,14 @@ int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_av
 int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers, const float* x,
                       const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
                       float* adam_state, int32_t* step, float lr, float beta1, float beta2,
-                      float eps, float* loss, float* logits, void* ws, void* stream) {
+                      float eps, float* loss, float* logits, void* ws, void* stream, int flags) {
     Geo g;
     if (int r = make_geo(dims, &g)) return r;
     if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
     if (int r = check_ptrs(x, "x", labels, "labels")) return r;
     if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
-    if (int r = check_ptrs(adam_state, "adam_state", step, "step")) return r;
+    if (adam_state && !step) return fail(EEGNET_EINVAL, "step is NULL");
+    g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
     g.drop = g.p > 0.f ? 1 : 0;
     g.key = mix_key(seed, offset);
     ensure_attrs();
@@ -1542,11 +1610,53 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
         ? run_backward<32>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, s)
         : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, s);
     if (r) return r;
+    if (!adam_state) return 0;       // gradients only (data-parallel: all-reduce, clamp, then Adam)
     return eegnet_adam_step(g.nparam, params, grads, adam_state, adam_state + g.nparam, step, lr,
                             beta1, beta2, eps, stream);
 }
 
+int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream) {
+    Geo g;
+    if (int r = make_geo(dims, &g, false)) return r;
+    if (!grads) return fail(EEGNET_EINVAL, "grads is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    const int n = std::max(g.F2 * g.C, NCLS * g.NF);
+    hipLaunchKernelGGL(k_clamp, dim3((n + NT - 1) / NT), dim3(NT), 0, s, g, grads);
+    LAUNCH_CHECK("k_clamp");
+    return 0;
+}
+
 const char* eegnet_last_error(void) { return g_err.c_str(); }
+
+int eegnet_profile_enable(int on) {
+    g_prof.on = on != 0;
+    return 0;
+}
+
+int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, int* n_out) {
+    double tot[KID_COUNT] = {0};
+    int cnt[KID_COUNT] = {0};
+    for (auto& r : g_prof.recs) {
+        hipEventSynchronize(r.b);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, r.a, r.b);
+        tot[r.kid] += ms;
+        cnt[r.kid] += 1;
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.recs.clear();
+    int n = 0;
+    for (int k = 0; k < KID_COUNT && n < cap; ++k) {
+        if (!cnt[k]) continue;
+        if (names) { strncpy(names + 32 * n, kKernelNames[k], 31); names[32 * n + 31] = 0; }
+        if (counts) counts[n] = cnt[k];
+        if (total_ms) total_ms[n] = tot[k];
+        ++n;
+    }
+    if (n_out) *n_out = n;
+    return 0;
+}
 
 const char* eegnet_build_info(void) {
     return "libeegnet_hip: gfx950 (CDNA4), fp32 VALU FIR/Gram + f32 MFMA 16x16x4 GEMMs, "

@@ -108,8 +108,11 @@ def forward_train(shape: Shape, flat_params, bn_flat, x, ws, seed: int, offset: 
     return logits
 
 
+NO_CLAMP = 1
+
+
 def backward(shape: Shape, flat_params, x, ws, seed: int, offset: int, dlogits=None, labels=None,
-             masks=None, p: float | None = None, grads=None, loss=None) -> torch.Tensor:
+             masks=None, p: float | None = None, grads=None, loss=None, clamp=True) -> torch.Tensor:
     B = x.shape[0]
     if grads is None:
         grads = torch.empty_like(flat_params)
@@ -118,8 +121,14 @@ def backward(shape: Shape, flat_params, x, ws, seed: int, offset: int, dlogits=N
     _lib.check(_lib.load().eegnet_backward(
         ctypes.byref(d), _ptr(flat_params), _ptr(x), _ptr(dlogits), _ptr(labels), _ptr(m2),
         _ptr(m3), ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(loss), _ptr(ws),
-        _stream()), "eegnet_backward")
+        _stream(), 0 if clamp else NO_CLAMP), "eegnet_backward")
     return grads
+
+
+def clamp_grads(shape: Shape, grads):
+    """model.py:44/84 gradient clamps on a flat grad buffer (after a data-parallel all-reduce)."""
+    _lib.check(_lib.load().eegnet_clamp_grads(ctypes.byref(shape.dims(1)), _ptr(grads), _stream()),
+               "eegnet_clamp_grads")
 
 
 def forward_eval(shape: Shape, flat_params, bn_flat, x) -> torch.Tensor:
@@ -141,11 +150,13 @@ def adam_step(params, grads, exp_avg, exp_avg_sq, step_i32, lr=1e-3, betas=(0.9,
 
 def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset: int, grads,
                adam_state, step_i32, ws, loss, logits=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-7,
-               p: float | None = None):
-    """One fused hot-loop iteration (model.py:141-148) on the device, no host sync."""
+               p: float | None = None, clamp=True):
+    """One fused hot-loop iteration (model.py:141-148) on the device, no host sync.
+    ``adam_state=None`` stops after the gradients (data-parallel)."""
     d = shape.dims(x.shape[0], p)
     _lib.check(_lib.load().eegnet_train_step(
         ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(labels),
         ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),
         _ptr(step_i32), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
-        ctypes.c_float(eps), _ptr(loss), _ptr(logits), _ptr(ws), _stream()), "eegnet_train_step")
+        ctypes.c_float(eps), _ptr(loss), _ptr(logits), _ptr(ws), _stream(),
+        0 if clamp else NO_CLAMP), "eegnet_train_step")

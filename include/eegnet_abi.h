@@ -58,6 +58,9 @@ enum {
 
 enum { EEGNET_TRAIN = 1, EEGNET_EVAL = 0 };
 
+/* eegnet_backward flags */
+enum { EEGNET_NO_CLAMP = 1 /* leave model.py:44/84 clamps to eegnet_clamp_grads (after an all-reduce) */ };
+
 /* Number of fp32 elements of the flat parameter buffer for these dims. */
 int eegnet_param_count(const eegnet_dims* dims, int64_t* out);
 
@@ -74,11 +77,15 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
  * Gradient source: `dlogits` [B,4] if non-NULL (autograd), else mean cross-entropy against `labels`
  * (train.py:103), in which case the scalar loss is written to `loss` (device fp32, nullable).
  * `grads` receives all 12 parameter gradients with the clamps of model.py:44 (+-1) and model.py:84
- * (+-0.25) applied. */
+ * (+-0.25) applied, unless flags has EEGNET_NO_CLAMP. */
 int eegnet_backward(const eegnet_dims* dims, const float* params, const float* x,
                     const float* dlogits, const int64_t* labels, const uint8_t* mask2,
                     const uint8_t* mask3, uint64_t seed, uint64_t offset, float* grads, float* loss,
-                    void* ws, void* stream);
+                    void* ws, void* stream, int flags);
+
+/* The gradient hooks of model.py:44 (spatial.weight, +-1) and model.py:84 (classifier.weight,
+ * +-0.25) on a flat grad buffer -- for data-parallel runs, after the gradient all-reduce. */
+int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream);
 
 /* Eval-mode forward (running statistics, no dropout): one fused kernel.  model.py:161/220, ui.py:35. */
 int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const float* bn_buffers,
@@ -91,11 +98,20 @@ int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_av
                      float eps, void* stream);
 
 /* One fused hot-loop iteration (model.py:141-148): forward_train + CE + backward + clamps + Adam.
- * adam_state = [exp_avg | exp_avg_sq] (2 * param_count floats); step as in eegnet_adam_step. */
+ * adam_state = [exp_avg | exp_avg_sq] (2 * param_count floats); step as in eegnet_adam_step.
+ * adam_state == NULL stops after the gradients (data-parallel callers all-reduce them, then call
+ * eegnet_clamp_grads and eegnet_adam_step); flags as for eegnet_backward.  logits is nullable. */
 int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers, const float* x,
                       const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
                       float* adam_state, int32_t* step, float lr, float beta1, float beta2,
-                      float eps, float* loss, float* logits, void* ws, void* stream);
+                      float eps, float* loss, float* logits, void* ws, void* stream, int flags);
+
+/* Optional per-kernel device timing for benchmarks: while enabled, every kernel this thread
+ * launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect synchronises
+ * them and reports, per kernel name (32-byte slots in `names`), launch count and summed device ms;
+ * it returns the number of kernels in *n_out.  Not for use under hipGraph capture. */
+int eegnet_profile_enable(int on);
+int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, int* n_out);
 
 /* Thread-local description of the last error ("" if none). */
 const char* eegnet_last_error(void);
