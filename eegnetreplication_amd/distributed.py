@@ -44,8 +44,21 @@ def init_process_group(backend: str | None = None):
     return rank, world, local
 
 
+def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place mean over ranks: ONE all-reduce of the whole flat buffer (latency-bound message)."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.mul_(1.0 / dist.get_world_size(group))
+    return t
+
+
 class DataParallelTrainer:
-    """Fused HIP train step + one RCCL gradient all-reduce per step (cfg4)."""
+    """Fused HIP train step + one RCCL gradient all-reduce per step (cfg4).
+
+    Per step: local gradients (HIP, clamps deferred) -> all-reduce mean -> model.py:44/84 clamps
+    -> Adam, replicated on every rank.  The three stages are methods so the orchestration can be
+    exercised on CPU (gloo) with a stand-in local step.
+    """
 
     def __init__(self, model: EEGNet, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, group=None):
         self.model = model
@@ -53,13 +66,16 @@ class DataParallelTrainer:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.adam = FusedAdamState(model)
         flat = model.flat_parameters()
         if self.world > 1:   # identical start on every rank
             dist.broadcast(flat, 0, group=group)
-        self.loss = torch.zeros(1, dtype=torch.float32, device=flat.device)
+        self._init_state(flat)
         self._ws = {}
         self._step = 0
+
+    def _init_state(self, flat):
+        self.adam = FusedAdamState(self.model)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=flat.device)
 
     def workspace(self, B):
         ws = self._ws.get(B)
@@ -68,25 +84,33 @@ class DataParallelTrainer:
             self._ws[B] = ws
         return ws
 
-    def step(self, x, y):
+    # -- stages ------------------------------------------------------------------------------
+    def local_grads(self, x, y, seed, offset):
         m = self.model
-        shape = m.shape
-        self._step += 1
-        seed = 0x5EED_0000 + self._step
-        offset = self._step * self.world + self.rank        # distinct masks on every rank
-        flat = m.flat_parameters()
-        grads = self.adam.grads
-        ops.train_step(shape, flat, m.flat_bn_buffers(), x, y, seed, offset, grads, None, None,
-                       self.workspace(x.shape[0]), self.loss, clamp=False)
-        if self.world > 1:
-            dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group)
-            grads.mul_(1.0 / self.world)
-        ops.clamp_grads(shape, grads)
+        ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
+                       self.adam.grads, None, None, self.workspace(x.shape[0]), self.loss,
+                       clamp=False)
+        for bn in m._bns():
+            bn.num_batches_tracked.add_(1)
+        return self.adam.grads
+
+    def clamp(self, grads):
+        ops.clamp_grads(self.model.shape, grads)
+
+    def update(self, grads):
+        flat = self.model.flat_parameters()
         n = flat.numel()
         ops.adam_step(flat, grads, self.adam.state[:n], self.adam.state[n:], self.adam.step,
                       lr=self.lr, betas=self.betas, eps=self.eps)
-        for bn in m._bns():
-            bn.num_batches_tracked.add_(1)
+
+    def step(self, x, y):
+        self._step += 1
+        seed = 0x5EED_0000 + self._step
+        offset = self._step * self.world + self.rank        # distinct masks on every rank
+        grads = self.local_grads(x, y, seed, offset)
+        allreduce_mean_(grads, self.group)
+        self.clamp(grads)
+        self.update(grads)
         return self.loss
 
 
