@@ -1,0 +1,243 @@
+// eegnet_common.h -- geometry, constants and device helpers shared by the EEGNet HIP kernels.
+// Part of the single translation unit built from eegnet_kernels.hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+namespace eeg {
+
+// One 1024-thread workgroup (16 waves of 64) per CU for the streaming passes.  A wave owns one
+// output row o of the per-trial [F2, T] planes, so row-wise work (FIR taps, reductions) is
+// wave-uniform: taps live in SGPRs and per-row partial sums stay in registers across trials.
+constexpr int NTH = 1024;
+constexpr int NWAVE = NTH / 64;
+constexpr int K2 = 16;        // block_2 depthwise taps (model.py:57)
+constexpr int NCLS = 4;       // classes (model.py:80)
+constexpr int LP2 = 8;        // left pad of d2 / dq rows in LDS (>= 7, multiple of 4)
+constexpr int MAXPF = 16;     // prefetch registers per thread: C*T <= NTH*MAXPF floats
+constexpr int F2MAX = 16;     // rows per trial plane this build keeps one-per-wave
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// Geometry shared by host and device (passed by value).  All LDS carve sizes come from the host.
+// ------------------------------------------------------------------------------------------------
+struct Geo {
+    int B, C, T, F1, D, F2, K1, P, R;
+    int T1, T2, NF;
+    int LP, RS;          // x / s / dy / e rows in LDS: left pad, row stride (floats, RS/4 odd)
+    int TQ, NT16;        // ceil(T/4) quads, ceil(T/16) MFMA column tiles
+    int RS2;             // block_2 rows (d2 / q / dq) stride
+    int CK, NCT, NKG;    // C padded to 4, ceil(C/16), ceil(T/16) k-groups of the dws GEMM
+    int nH, nTl, nedge;  // lag-Gram edge terms: head pairs R(R+1)/2, tail pairs P(P+1)/2, + R + P sums
+    float p, scale, eps, mom;
+    int drop;
+    int xdb;             // pass E: double-buffered x rows
+    int noclamp;         // skip the model.py:44/84 clamps (data-parallel: clamp after all-reduce)
+    unsigned long long key;
+    // flat parameter offsets (named_parameters order)
+    int o_w1, o_g1, o_b1, o_ws, o_g2, o_b2, o_w2, o_W3, o_g3, o_b3, o_Wfc, o_bfc, nparam;
+    // partial-row lengths of the five passes and the (common) workgroup count
+    int nA, nB, nC, nD, nE;
+    int grid;
+    // LDS (floats)
+    int ldsA, ldsB, ldsC, ldsD, ldsE, ldsI;
+};
+
+// coefficient block layout (float, CSTR per field; F1, F2 <= 64)
+enum CoefField {
+    CF_A1 = 0, CF_C1, CF_INV1, CF_MU1, CF_AL2, CF_BE2, CF_INV2, CF_MU3, CF_INV3,
+    CF_A3, CF_B3, CF_C3, CF_AO, CF_BO, CF_CO, CF_W, CF_LOSS, CF_COUNT
+};
+constexpr int CSTR = 64;
+
+enum PassCMode { PC_LOGITS = 1, PC_BWD = 2, PC_CE = 4 };
+
+// padded-row strides, shared by host (make_geo) and the compile-time-shape kernels
+__host__ __device__ constexpr int rup4(int a) { return (a + 3) & ~3; }
+__host__ __device__ constexpr int imax(int a, int b) { return a > b ? a : b; }
+__host__ __device__ constexpr int row_stride(int K1, int T) {
+    // rows of x / s / dy / e: [LP zeros | T samples | >= R zeros]; long enough for the last 4-output
+    // FIR window and the last 16-column MFMA tile; RS/4 odd so that column reads of 16 rows (MFMA
+    // operands) land in 16 different bank groups
+    const int P = (K1 - 1) / 2, R = K1 - 1 - P, LP = (R + 3) & ~3, OFF = LP - P;
+    const int NW = (OFF + K1 + 6) / 4, TQ = (T + 3) / 4, NT16 = (T + 15) / 16;
+    const int rs = rup4(imax(imax(4 * (TQ - 1) + 4 * NW, LP + 16 * NT16), LP + T + R));
+    return ((rs / 4) & 1) ? rs : rs + 4;
+}
+__host__ __device__ constexpr int row_stride2(int T) { return rup4(LP2 + T / 4 + 8); }
+
+// compile-time row geometry for a temporal kernel length
+template <int K1>
+struct KG {
+    static constexpr int P = (K1 - 1) / 2;          // left 'same' pad (model.py:27)
+    static constexpr int R = K1 - 1 - P;            // right pad
+    static constexpr int LP = (R + 3) & ~3;         // LDS left pad (>= P, >= R, multiple of 4)
+    static constexpr int OFF = LP - P;              // window offset of the forward FIR / Gram
+    static constexpr int OFFD = LP - R;             // window offset of the transposed FIR
+    static constexpr int NW = (OFF + K1 + 3 + 3) / 4;   // float4s per 4-output window
+    static constexpr int NEI = ((R * (R + 1) / 2 + P * (P + 1) / 2 + R + P) + NTH - 1) / NTH;
+};
+
+// ------------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : expm1f(z); }
+__device__ __forceinline__ float elu_d(float z) { return z > 0.f ? 1.f : expf(z); }
+
+// Dropout keep factor (model.py:50,74 nn.Dropout: x * mask / (1-p)).  Injected masks win; otherwise a
+// counter-based splitmix64 draw keyed by (key, layer, flat index) -- identical in forward and backward.
+__device__ __forceinline__ float keep_mul(const Geo& g, const uint8_t* __restrict__ mask, int layer,
+                                          unsigned long long idx) {
+    if (!g.drop) return 1.f;
+    if (mask) return mask[idx] ? g.scale : 0.f;
+    unsigned long long z = g.key + ((unsigned long long)(layer + 1) << 56) + idx * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const float u = (float)(unsigned)(z >> 40) * (1.0f / 16777216.0f);
+    return u >= g.p ? g.scale : 0.f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// order this wave's LDS writes before its later LDS reads (rows a wave owns need no block barrier)
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// NW aligned float4 loads from LDS (p must be 16-byte aligned: row base + multiple of 4 floats)
+template <int NW>
+__device__ __forceinline__ void lds_window(const float* __restrict__ p, float (&w)[4 * NW]) {
+    const float4* p4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(p, 16));
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const float4 f = p4[i];
+        w[4 * i + 0] = f.x; w[4 * i + 1] = f.y; w[4 * i + 2] = f.z; w[4 * i + 3] = f.w;
+    }
+}
+
+// 4 outputs of a K-tap correlation from a window: out[i] = sum_k tap[k] * w[OFF + i + k]
+template <int K, int OFF, int NWF>
+__device__ __forceinline__ void fir4(const float (&w)[NWF], const float (&tap)[K], float (&out)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) a = fmaf(tap[k], w[OFF + i + k], a);
+        out[i] = a;
+    }
+}
+
+// ---- x staging: global -> registers (issued a whole trial ahead) -> LDS rows ----
+// PF floats per thread cover one trial: C*T <= NTH*PF.
+template <int PF>
+__device__ __forceinline__ void x_prefetch(const float* __restrict__ xb, int C, int T, float (&pf)[PF], int tid) {
+    const int n = C * T;
+    if ((T & 3) == 0) {
+        const float4* src = reinterpret_cast<const float4*>(xb);
+#pragma unroll
+        for (int j = 0; j < PF / 4; ++j) {
+            const int i = tid + NTH * j;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (4 * i < n) v = src[i];
+            pf[4 * j] = v.x; pf[4 * j + 1] = v.y; pf[4 * j + 2] = v.z; pf[4 * j + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            const int i = tid + NTH * j;
+            pf[j] = i < n ? xb[i] : 0.f;
+        }
+    }
+}
+
+template <int PF>
+__device__ __forceinline__ void x_store(const float (&pf)[PF], int C, int T, int RS, int LP, float* Xs, int tid) {
+    const int n = C * T;
+    if ((T & 3) == 0) {
+        const int TQ = T >> 2;
+#pragma unroll
+        for (int j = 0; j < PF / 4; ++j) {
+            const int i = tid + NTH * j;
+            if (4 * i < n) {
+                const int c = i / TQ, q = i - c * TQ;
+                *reinterpret_cast<float4*>(Xs + c * RS + LP + 4 * q) =
+                    make_float4(pf[4 * j], pf[4 * j + 1], pf[4 * j + 2], pf[4 * j + 3]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            const int i = tid + NTH * j;
+            if (i < n) {
+                const int c = i / T, t = i - c * T;
+                Xs[c * RS + LP + t] = pf[j];
+            }
+        }
+    }
+}
+
+// spatial A operand (ws, 16 o x 4 c per k-step) kept in registers for the whole workgroup:
+// lane l holds ws[o = l&15][c = 4s + (l>>4)] for k-step s (zero outside F2 x C); KS = ceil(C/4)
+template <int KS>
+__device__ __forceinline__ void load_ws_frag(const float* __restrict__ ws, int C, int F2, float (&aw)[KS],
+                                             int lane) {
+    const int o = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int c = 4 * s + lk;
+        aw[s] = (o < F2 && c < C) ? ws[o * C + c] : 0.f;
+    }
+}
+
+// s[o,t] = sum_c ws[o,c] x[c,t] on the matrix cores: v_mfma_f32_16x16x4_f32, A = ws (registers),
+// B = x tile (4 c x 16 t).  Lane l: A[l&15][l>>4], B[l>>4][l&15]; D[4(l>>4)+r][l&15] (CDNA4 maps).
+// Exact f32 (a k-ordered fmaf chain).  Wave w computes column tiles w, w+16, ...
+template <int KS>
+__device__ __forceinline__ void spatial_mfma(const float* Xs, const float (&aw)[KS], float* Ss, int C, int F2,
+                                             int NT16, int RS, int LP, int wave, int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+    const int ks = (C + 3) >> 2;
+    for (int n = wave; n < NT16; n += NWAVE) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* xcol = Xs + lk * RS + LP + 16 * n + li;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            if (s < ks) {
+                const int c = 4 * s + lk;
+                const float b = (c < C) ? xcol[4 * s * RS] : 0.f;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aw[s], b, acc, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = 4 * lk + r;
+            if (o < F2) Ss[o * RS + LP + 16 * n + li] = acc[r];
+        }
+    }
+}
+
+// Static shape of a kernel instantiation: CC/TT/FF = 0 means "runtime value from Geo".
+#define EEG_DIMS(g)                                                                         \
+    const int C = CC ? CC : (g).C;                                                          \
+    const int T = TT ? TT : (g).T;                                                          \
+    const int F2 = FF ? FF : (g).F2;                                                        \
+    const int TQ = (T + 3) >> 2, T1 = T >> 2, T2 = T1 >> 3, NF = F2 * T2;                   \
+    const int RS = TT ? row_stride(K1, TT) : (g).RS;                                        \
+    const int RS2 = TT ? row_stride2(TT) : (g).RS2;                                         \
+    const int NT16 = (T + 15) >> 4, NCT = (C + 15) >> 4;                                    \
+    constexpr int LP = KG<K1>::LP;                                                          \
+    constexpr int PF = (CC && TT) ? ((CC * TT + NTH - 1) / NTH + 3) / 4 * 4 : 16;            \
+    constexpr int KS = CC ? (CC + 3) / 4 : 16;                                              \
+    (void)TQ; (void)T1; (void)T2; (void)NF; (void)RS2; (void)NT16; (void)NCT; (void)LP
+
+}  // namespace eeg

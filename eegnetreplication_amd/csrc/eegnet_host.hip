@@ -1,0 +1,458 @@
+// eegnet_host.hip -- host side of libeegnet_hip.so: geometry/validation, workspace layout, launch
+// sequences of the train step and the C-ABI of include/eegnet_abi.h.  Included by eegnet_kernels.hip.
+// ================================================================================================
+// Host side: geometry, validation, launch sequences, C-ABI.
+// ================================================================================================
+using namespace eeg;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+static inline int rup(int a, int m) { return (a + m - 1) / m * m; }
+static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
+
+struct WsLayout {
+    size_t partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, total;
+};
+
+static int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;     // MI355X
+    }
+    return cus;
+}
+
+static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
+    if (!d) return fail(EEGNET_EINVAL, "dims is NULL");
+    memset(g, 0, sizeof(*g));
+    g->B = d->B; g->C = d->C; g->T = d->T; g->F1 = d->F1; g->D = d->D; g->K1 = d->K1;
+    g->F2 = d->F1 * d->D;
+    if (g->B < 1) return fail(EEGNET_EINVAL, "B must be >= 1 (got %d)", g->B);
+    if (g->K1 != 32 && g->K1 != 64) return fail(EEGNET_EINVAL, "K1 must be 32 or 64 (got %d)", g->K1);
+    if (g->C < 1 || g->C > 64) return fail(EEGNET_EINVAL, "C must be in [1,64] (got %d)", g->C);
+    if (g->F1 < 1 || g->D < 1 || g->F2 > 64 || (g->F2 & 3))
+        return fail(EEGNET_EINVAL, "F1*D must be a multiple of 4 in [4,64] (got F1=%d D=%d)", g->F1, g->D);
+    if (g->T < 32 || g->T < g->K1 || g->T > 1024)
+        return fail(EEGNET_EINVAL, "T must be in [max(32,K1), 1024] (got %d)", g->T);
+    g->P = (g->K1 - 1) / 2; g->R = g->K1 - 1 - g->P;
+    g->T1 = g->T / 4; g->T2 = g->T1 / 8; g->NF = g->F2 * g->T2;
+    g->LP = (g->R + 3) & ~3;
+    g->TQ = (g->T + 3) / 4; g->NT16 = (g->T + 15) / 16; g->NKG = g->NT16;
+    {
+        const int OFF = g->LP - g->P;
+        const int NW = (OFF + g->K1 + 6) / 4;
+        int rs = std::max(4 * (g->TQ - 1) + 4 * NW, g->LP + 16 * g->NT16);
+        rs = std::max(rs, g->LP + g->T + g->R);
+        rs = rup(rs, 4);
+        if (((rs / 4) & 1) == 0) rs += 4;      // RS/4 odd: column reads of 16 rows hit 16 banks
+        g->RS = rs;
+    }
+    g->RS2 = rup(LP2 + g->T1 + 8, 4);
+    g->CK = rup(g->C, 4); g->NCT = (g->C + 15) / 16;
+    g->nH = g->R * (g->R + 1) / 2;
+    g->nTl = g->P * (g->P + 1) / 2;
+    g->nedge = g->nH + g->nTl + g->R + g->P;
+    g->p = d->p_drop; g->eps = d->bn_eps; g->mom = d->bn_momentum;
+    if (!(g->p >= 0.f && g->p <= 1.f)) return fail(EEGNET_EINVAL, "p_drop must be in [0,1]");
+    g->scale = g->p < 1.f ? 1.f / (1.f - g->p) : 0.f;
+    int o = 0;
+    g->o_w1 = o; o += g->F1 * g->K1;
+    g->o_g1 = o; o += g->F1;
+    g->o_b1 = o; o += g->F1;
+    g->o_ws = o; o += g->F2 * g->C;
+    g->o_g2 = o; o += g->F2;
+    g->o_b2 = o; o += g->F2;
+    g->o_w2 = o; o += g->F2 * 16;
+    g->o_W3 = o; o += g->F2 * g->F2;
+    g->o_g3 = o; o += g->F2;
+    g->o_b3 = o; o += g->F2;
+    g->o_Wfc = o; o += NCLS * g->NF;
+    g->o_bfc = o; o += NCLS;
+    g->nparam = o;
+    if (g->NF < 1) return fail(EEGNET_EINVAL, "T//32 must be >= 1");
+    g->nA = g->K1 + 1 + g->nedge + 2 * g->F2;
+    g->nB = 2 * g->F2;
+    g->nC = NCLS * g->NF + NCLS + 2 * g->F2 + 1;
+    g->nD = g->F2 * g->F2 + 18 * g->F2;
+    g->nE = g->F2 * g->K1 + g->F2 * g->C + 2 * g->F2;
+    g->grid = std::min(g->B, device_cus());
+    const int rows1 = g->C * g->RS;                   // x rows (A, B, infer: one buffer)
+    const int rows2 = 2 * g->C * g->RS;               // double-buffered x rows (E)
+    const int nf4 = rup(g->NF, 4);
+    g->ldsA = rows1 + g->F2 * g->RS + NWAVE * (g->K1 + 1);
+    g->ldsB = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2;
+    g->ldsC = 2 * g->F2 * g->RS2 + 2 * nf4 + 8;
+    g->ldsD = 4 * g->F2 * g->RS2 + nf4;
+    g->ldsE = 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4);
+    g->xdb = (g->ldsE + rows2) * 4 <= 160 * 1024 ? 1 : 0;
+    g->ldsE = std::max(g->ldsE + (g->xdb ? rows2 : rows1), NWAVE * 256);
+    g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
+    if (launch) {
+        if (g->F2 > F2MAX)
+            return fail(EEGNET_EINVAL, "F1*D = %d > %d: the row-per-wave train step covers F2 <= %d "
+                        "(EEGNet-16,4 needs the cfg5 kernels)", g->F2, F2MAX, F2MAX);
+        if (g->C * g->T > NTH * MAXPF)
+            return fail(EEGNET_EINVAL, "C*T = %d exceeds the %d-float prefetch of one trial", g->C * g->T,
+                        NTH * MAXPF);
+        if (g->T1 > 64 * MAXT1Q) return fail(EEGNET_EINVAL, "T/4 > %d", 64 * MAXT1Q);
+        if (NCLS * g->NF > 4 * NTH) return fail(EEGNET_EINVAL, "F2*(T/32) too large");
+        const int lmax = std::max(std::max(std::max(g->ldsA, g->ldsB), std::max(g->ldsC, g->ldsD)),
+                                  std::max(g->ldsE, g->ldsI));
+        if (lmax * 4 > 160 * 1024) return fail(EEGNET_EINVAL, "dims need %d B of LDS (> 160 KiB)", lmax * 4);
+    }
+    return 0;
+}
+
+static WsLayout make_layout(const Geo& g) {
+    WsLayout L;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = rupz(o + bytes, 256); return r; };
+    L.partA = take((size_t)g.grid * g.nA * 4);
+    L.partB = take((size_t)g.grid * g.nB * 4);
+    L.partC = take((size_t)g.grid * g.nC * 4);
+    L.partD = take((size_t)g.grid * g.nD * 4);
+    L.partE = take((size_t)g.grid * g.nE * 4);
+    const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
+    L.sums = take((size_t)nmax * 8 * RCH);
+    L.stats = take((size_t)(g.K1 * g.K1 + g.K1) * 8);
+    L.coef = take((size_t)CF_COUNT * CSTR * 4);
+    const size_t per = (size_t)g.B * g.F2 * g.T1 * 4;
+    L.d2 = take(per); L.E1 = take(per); L.E2 = take(per); L.dp2 = take(per);
+    L.dl = take((size_t)g.B * NCLS * 4);
+    L.total = o;
+    return L;
+}
+
+static uint64_t mix_key(uint64_t seed, uint64_t offset) {
+    uint64_t z = seed * 0xD1B54A32D192ED03ull + offset * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ---- optional per-kernel device timing (bench / roofline), off by default ----
+enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_COLSUM, KID_FIN, KID_ADAM, KID_INFER, KID_COUNT };
+static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
+                                              "k_colsum", "k_fin", "k_adam", "k_infer"};
+struct ProfRec { int kid; hipEvent_t a, b; };
+struct ProfState { bool on = false; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
+static thread_local ProfState g_prof;
+
+static hipEvent_t prof_event() {
+    if (!g_prof.pool.empty()) { hipEvent_t e = g_prof.pool.back(); g_prof.pool.pop_back(); return e; }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+struct ProfScope {
+    int kid; hipStream_t s; hipEvent_t a = nullptr;
+    ProfScope(int k, hipStream_t st) : kid(k), s(st) {
+        if (g_prof.on) { a = prof_event(); hipEventRecord(a, s); }
+    }
+    ~ProfScope() {
+        if (a) { hipEvent_t b = prof_event(); hipEventRecord(b, s); g_prof.recs.push_back({kid, a, b}); }
+    }
+};
+#define PROF(kid) ProfScope prof_scope_##kid(kid, s)
+
+#define LAUNCH_CHECK(what)                                                            \
+    do {                                                                              \
+        hipError_t e_ = hipGetLastError();                                            \
+        if (e_ != hipSuccess) return fail(EEGNET_ELAUNCH, "%s: %s", what, hipGetErrorString(e_)); \
+    } while (0)
+
+static bool g_attr_done = false;
+
+template <int K1, int CC, int TT, int FF>
+static void set_attrs_shape() {
+    const int lds = 160 * 1024;
+    hipFuncSetAttribute((const void*)k_pass_a<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute((const void*)k_pass_b<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute((const void*)k_pass_c<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute((const void*)k_pass_d<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute((const void*)k_pass_e<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute((const void*)k_infer<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+static void ensure_attrs() {
+    if (g_attr_done) return;
+    set_attrs_shape<32, 0, 0, 0>();
+    set_attrs_shape<64, 0, 0, 0>();
+    set_attrs_shape<32, 22, 256, 16>();
+    set_attrs_shape<32, 22, 257, 16>();
+    hipFuncSetAttribute((const void*)k_fin1, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    g_attr_done = true;
+}
+
+// compile-time shape specialisations (the benchmark and real-data configurations); any other shape
+// runs the runtime-shape instantiation of the same kernels
+#define EEG_DISPATCH(K1_, g_, LAUNCH)                                                            \
+    do {                                                                                         \
+        if ((K1_) == 32 && (g_).C == 22 && (g_).T == 256 && (g_).F2 == 16) { LAUNCH(32, 22, 256, 16); } \
+        else if ((K1_) == 32 && (g_).C == 22 && (g_).T == 257 && (g_).F2 == 16) { LAUNCH(32, 22, 257, 16); } \
+        else { LAUNCH(K1_, 0, 0, 0); }                                                           \
+    } while (0)
+
+static int colsum(const float* part, int nrows, int ncols, double* out, hipStream_t s) {
+    PROF(KID_COLSUM);
+    hipLaunchKernelGGL(k_colsum, dim3((ncols + 63) / 64, RCH), dim3(256), 0, s, part, nrows, ncols, out);
+    LAUNCH_CHECK("k_colsum");
+    return 0;
+}
+
+template <int K1>
+static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
+                       const float* x, const uint8_t* m2, float* logits, int update_running,
+                       int c_mode, const int64_t* labels, float* loss, float* grads, hipStream_t s) {
+    double* sums = (double*)(ws + L.sums);
+    float* coef = (float*)(ws + L.coef);
+#define LAUNCH_A(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsA * 4, s, \
+                                                   g, params, x, (float*)(ws + L.partA))
+    { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
+    } LAUNCH_CHECK("k_pass_a");
+    if (int r = colsum((float*)(ws + L.partA), g.grid, g.nA, sums, s)) return r;
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin1, dim3(1), dim3(256), (g.K1 * g.K1 + g.K1 + 128 + g.nA) * 8, s, g, params, sums,
+                       (double*)(ws + L.stats), coef, bn, update_running);
+    } LAUNCH_CHECK("k_fin1");
+#define LAUNCH_B(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsB * 4, s, \
+                       g, params, coef, x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), (float*)(ws + L.E2), \
+                       (float*)(ws + L.partB))
+    { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
+    } LAUNCH_CHECK("k_pass_b");
+    if (int r = colsum((float*)(ws + L.partB), g.grid, g.nB, sums, s)) return r;
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin2, dim3(1), dim3(256), g.nB * 8, s, g, sums, coef, bn, update_running);
+    } LAUNCH_CHECK("k_fin2");
+    (void)labels; (void)loss; (void)grads; (void)c_mode; (void)logits;
+    return 0;
+}
+
+template <int K1>
+static int run_backward(const Geo& g, const WsLayout& L, char* ws, const float* params,
+                        const float* x, const uint8_t* m2, const uint8_t* m3, const float* dlogits,
+                        const int64_t* labels, float* logits, float* grads, float* loss, int c_mode,
+                        hipStream_t s) {
+    double* sums = (double*)(ws + L.sums);
+    float* coef = (float*)(ws + L.coef);
+    float* dl = dlogits ? (float*)dlogits : (float*)(ws + L.dl);
+#define LAUNCH_CB(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsC * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
+                       (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode)
+    { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
+    } LAUNCH_CHECK("k_pass_c(bwd)");
+    if (int r = colsum((float*)(ws + L.partC), g.grid, g.nC, sums, s)) return r;
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin3, dim3(1), dim3(256), g.nC * 8, s, g, params, sums, coef, grads, loss,
+                       (c_mode & PC_CE) ? 1 : 0);
+    } LAUNCH_CHECK("k_fin3");
+#define LAUNCH_D(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsD * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
+                       (const float*)(ws + L.E2), m2, m3, (const float*)dl, (float*)(ws + L.dp2), \
+                       (float*)(ws + L.partD))
+    { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
+    } LAUNCH_CHECK("k_pass_d");
+    if (int r = colsum((float*)(ws + L.partD), g.grid, g.nD, sums, s)) return r;
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin4, dim3(1), dim3(256), g.nD * 8, s, g, params, sums, coef, grads);
+    } LAUNCH_CHECK("k_fin4");
+#define LAUNCH_E(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsE * 4, s, \
+                       g, params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE))
+    { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
+    } LAUNCH_CHECK("k_pass_e");
+    if (int r = colsum((float*)(ws + L.partE), g.grid, g.nE, sums, s)) return r;
+    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin5, dim3(1), dim3(256), g.nE * 8, s, g, params, sums, (const double*)(ws + L.stats),
+                       (const float*)coef, grads);
+    } LAUNCH_CHECK("k_fin5");
+    return 0;
+}
+
+static int check_ptrs(const void* a, const char* na, const void* b = (const void*)1, const char* nb = "") {
+    if (!a) return fail(EEGNET_EINVAL, "%s is NULL", na);
+    if (!b) return fail(EEGNET_EINVAL, "%s is NULL", nb);
+    return 0;
+}
+
+extern "C" {
+
+int eegnet_param_count(const eegnet_dims* dims, int64_t* out) {
+    Geo g;
+    if (int r = make_geo(dims, &g, false)) return r;
+    if (!out) return fail(EEGNET_EINVAL, "out is NULL");
+    *out = g.nparam;
+    return 0;
+}
+
+int eegnet_workspace_bytes(const eegnet_dims* dims, size_t* out) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (!out) return fail(EEGNET_EINVAL, "out is NULL");
+    *out = make_layout(g).total;
+    return 0;
+}
+
+int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn_buffers,
+                         const float* x, const uint8_t* mask2, const uint8_t* mask3,
+                         uint64_t seed, uint64_t offset, float* logits, void* ws, void* stream) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
+    if (int r = check_ptrs(x, "x", logits, "logits")) return r;
+    if (int r = check_ptrs(ws, "ws")) return r;
+    g.drop = g.p > 0.f ? 1 : 0;
+    g.key = mix_key(seed, offset);
+    ensure_attrs();
+    const WsLayout L = make_layout(g);
+    hipStream_t s = (hipStream_t)stream;
+    char* w = (char*)ws;
+    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, mask2, logits, 1, 0, nullptr, nullptr, nullptr, s)
+                       : run_forward<64>(g, L, w, params, bn_buffers, x, mask2, logits, 1, 0, nullptr, nullptr, nullptr, s);
+    if (r) return r;
+#define LAUNCH_CF(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsC * 4, s, \
+                       g, params, (const float*)(w + L.coef), (const float*)(w + L.d2), mask3, (const float*)nullptr, \
+                       (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS)
+    { PROF(KID_C);
+      if (g.K1 == 32) EEG_DISPATCH(32, g, LAUNCH_CF); else EEG_DISPATCH(64, g, LAUNCH_CF);
+    } LAUNCH_CHECK("k_pass_c(fwd)");
+    return 0;
+}
+
+int eegnet_backward(const eegnet_dims* dims, const float* params, const float* x,
+                    const float* dlogits, const int64_t* labels, const uint8_t* mask2,
+                    const uint8_t* mask3, uint64_t seed, uint64_t offset, float* grads, float* loss,
+                    void* ws, void* stream, int flags) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
+    if (int r = check_ptrs(params, "params", x, "x")) return r;
+    if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
+    if (!dlogits && !labels) return fail(EEGNET_EINVAL, "need dlogits or labels");
+    g.drop = g.p > 0.f ? 1 : 0;
+    g.key = mix_key(seed, offset);
+    ensure_attrs();
+    const WsLayout L = make_layout(g);
+    const int mode = PC_BWD | (dlogits ? 0 : PC_CE);
+    hipStream_t s = (hipStream_t)stream;
+    return g.K1 == 32
+        ? run_backward<32>(g, L, (char*)ws, params, x, mask2, mask3, dlogits, labels, nullptr, grads, loss, mode, s)
+        : run_backward<64>(g, L, (char*)ws, params, x, mask2, mask3, dlogits, labels, nullptr, grads, loss, mode, s);
+}
+
+int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const float* bn_buffers,
+                        const float* x, float* logits, void* stream) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
+    if (int r = check_ptrs(x, "x", logits, "logits")) return r;
+    ensure_attrs();
+    hipStream_t s = (hipStream_t)stream;
+    PROF(KID_INFER);
+#define LAUNCH_I(K, CC, TT, FF) hipLaunchKernelGGL((k_infer<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsI * 4, s, \
+                                                   g, params, bn_buffers, x, logits)
+    if (g.K1 == 32) EEG_DISPATCH(32, g, LAUNCH_I); else EEG_DISPATCH(64, g, LAUNCH_I);
+    LAUNCH_CHECK("k_infer");
+    return 0;
+}
+
+int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_avg,
+                     float* exp_avg_sq, int32_t* step, float lr, float beta1, float beta2,
+                     float eps, void* stream) {
+    if (n <= 0) return fail(EEGNET_EINVAL, "n must be > 0");
+    if (!params || !grads || !exp_avg || !exp_avg_sq || !step) return fail(EEGNET_EINVAL, "null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    { PROF(KID_ADAM); hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, params, grads,
+                       exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps);
+    } LAUNCH_CHECK("k_adam");
+    hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(64), 0, s, step);
+    LAUNCH_CHECK("k_step_inc");
+    return 0;
+}
+
+int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers, const float* x,
+                      const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
+                      float* adam_state, int32_t* step, float lr, float beta1, float beta2,
+                      float eps, float* loss, float* logits, void* ws, void* stream, int flags) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
+    if (int r = check_ptrs(x, "x", labels, "labels")) return r;
+    if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
+    if (adam_state && !step) return fail(EEGNET_EINVAL, "step is NULL");
+    g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
+    g.drop = g.p > 0.f ? 1 : 0;
+    g.key = mix_key(seed, offset);
+    ensure_attrs();
+    const WsLayout L = make_layout(g);
+    hipStream_t s = (hipStream_t)stream;
+    char* w = (char*)ws;
+    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, nullptr, 1, 0, nullptr, nullptr, nullptr, s)
+                       : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, nullptr, 1, 0, nullptr, nullptr, nullptr, s);
+    if (r) return r;
+    const int mode = PC_BWD | PC_CE | (logits ? PC_LOGITS : 0);
+    r = g.K1 == 32
+        ? run_backward<32>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, s)
+        : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, s);
+    if (r) return r;
+    if (!adam_state) return 0;       // gradients only (data-parallel: all-reduce, clamp, then Adam)
+    return eegnet_adam_step(g.nparam, params, grads, adam_state, adam_state + g.nparam, step, lr,
+                            beta1, beta2, eps, stream);
+}
+
+int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream) {
+    Geo g;
+    if (int r = make_geo(dims, &g, false)) return r;
+    if (!grads) return fail(EEGNET_EINVAL, "grads is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    const int n = std::max(g.F2 * g.C, NCLS * g.NF);
+    hipLaunchKernelGGL(k_clamp, dim3((n + 255) / 256), dim3(256), 0, s, g, grads);
+    LAUNCH_CHECK("k_clamp");
+    return 0;
+}
+
+const char* eegnet_last_error(void) { return g_err.c_str(); }
+
+int eegnet_profile_enable(int on) {
+    g_prof.on = on != 0;
+    return 0;
+}
+
+int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, int* n_out) {
+    double tot[KID_COUNT] = {0};
+    int cnt[KID_COUNT] = {0};
+    for (auto& r : g_prof.recs) {
+        hipEventSynchronize(r.b);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, r.a, r.b);
+        tot[r.kid] += ms;
+        cnt[r.kid] += 1;
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.recs.clear();
+    int n = 0;
+    for (int k = 0; k < KID_COUNT && n < cap; ++k) {
+        if (!cnt[k]) continue;
+        if (names) { strncpy(names + 32 * n, kKernelNames[k], 31); names[32 * n + 31] = 0; }
+        if (counts) counts[n] = cnt[k];
+        if (total_ms) total_ms[n] = tot[k];
+        ++n;
+    }
+    if (n_out) *n_out = n;
+    return 0;
+}
+
+const char* eegnet_build_info(void) {
+    return "libeegnet_hip: gfx950 (CDNA4), fp32 VALU FIR/Gram + f32 MFMA 16x16x4 GEMMs, "
+           "5-pass restructured EEGNet train step, 1024-thread row-per-wave workgroups";
+}
+
+}  // extern "C"

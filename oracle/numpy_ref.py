@@ -247,8 +247,9 @@ def cross_entropy(logits: np.ndarray, labels: np.ndarray):
     return loss, dz / B
 
 
-def backward(cache: dict, dlogits: np.ndarray) -> dict:
-    """loss.backward() through EEGNet, including the two gradient clamps (model.py:44,84).
+def backward(cache: dict, dlogits: np.ndarray, clamp: bool = True) -> dict:
+    """loss.backward() through EEGNet, including the two gradient clamps (model.py:44,84);
+    ``clamp=False`` returns the raw gradients (the scale the clamp is applied at).
 
     Returns grads keyed by parameter name, shaped like the parameters.
     """
@@ -259,7 +260,7 @@ def backward(cache: dict, dlogits: np.ndarray) -> dict:
     dz = np.asarray(dlogits, dtype=np.float64)
     g = {}
     h = cache["h"]
-    g["classifier.weight"] = np.clip(dz.T @ h, -CLASSIFIER_CLAMP, CLASSIFIER_CLAMP)
+    g["classifier.weight"] = np.clip(dz.T @ h, -CLASSIFIER_CLAMP, CLASSIFIER_CLAMP) if clamp else dz.T @ h
     g["classifier.bias"] = dz.sum(axis=0)
     dh = dz @ P["classifier.weight"]
     dd3 = dh.reshape(B, F2, dm.T2)
@@ -283,7 +284,7 @@ def backward(cache: dict, dlogits: np.ndarray) -> dict:
     y1 = cache["y1"]
     grp = cache["grp"]
     dws = np.einsum("bot,boct->oc", dy2, y1[:, grp, :, :])
-    g["spatial.weight"] = np.clip(dws, -SPATIAL_CLAMP, SPATIAL_CLAMP).reshape(F2, 1, C, 1)
+    g["spatial.weight"] = (np.clip(dws, -SPATIAL_CLAMP, SPATIAL_CLAMP) if clamp else dws).reshape(F2, 1, C, 1)
     ws = P["spatial.weight"].reshape(F2, C)
     dy1 = np.zeros((B, F1, C, T))
     for o in range(F2):
