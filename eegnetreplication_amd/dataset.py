@@ -1,0 +1,127 @@
+"""Data feed for the EEGNet step.
+
+* ``BCICI2ADataset`` -- the reference's Dataset type (dataset.py:30-43): ``X[n,C,T]`` float64,
+  ``y[n]`` int, ``__getitem__ -> (X[i], int(y[i]))``.
+* ``build_dataset_from_preprocessed(subject, mode)`` -- same call as the reference
+  (dataset.py:239-281).  The reference epochs MNE/braindecode-preprocessed GDF recordings; those
+  libraries and the BCI IV-2a files are not available offline, so this build loads
+  ``data/processed/A0{subject}{T|E}.npz`` (arrays ``X``, ``y``) when present and otherwise generates
+  a seeded synthetic motor-imagery-like session with the real shape: 288 trials x 22 channels x
+  257 samples (128 Hz, 0.5-2.5 s), 4 balanced classes.
+* ``DeviceLoader`` -- a device-resident replacement for ``DataLoader(batch_size, shuffle)``: the
+  whole split is cast to fp32 and moved to HBM once; batches are index_select views, so the hot
+  loop has no per-batch host->device copy (the reference copies every batch, model.py:138).
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+N_CHANNELS = 22
+N_SAMPLES = 257
+SFREQ = 128.0
+TRIALS_PER_SESSION = 288
+# 10-20 positions of the BCI IV-2a montage used for the class-dependent rhythms
+C3, CZ, C4 = 7, 9, 11
+
+
+@dataclass(frozen=True)
+class BCICI2ADataset(torch.utils.data.Dataset):
+    """dataset.py:30-43: X [n, C, T] float64, y [n] int."""
+    X: np.ndarray
+    y: np.ndarray
+
+    def __len__(self):
+        return len(self.y)
+
+    def __getitem__(self, i):
+        return self.X[i], int(self.y[i])
+
+
+def _pink_noise(rng, shape, T):
+    """1/f noise along the last axis (spectral shaping of white noise)."""
+    white = rng.standard_normal(shape[:-1] + (T,))
+    f = np.fft.rfftfreq(T, d=1.0 / SFREQ)
+    scale = 1.0 / np.sqrt(np.maximum(f, 1.0))
+    return np.fft.irfft(np.fft.rfft(white, axis=-1) * scale, n=T, axis=-1)
+
+
+def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C=N_CHANNELS,
+                      T=N_SAMPLES) -> BCICI2ADataset:
+    """Seeded SMR-like session: classes 0..3 = left hand / right hand / feet /
+    tongue.  Hand imagery desynchronises the mu (8-12 Hz) and beta (18-26 Hz) rhythm over the
+    contralateral sensorimotor cortex (C4 for left, C3 for right), feet over Cz, tongue weakly
+    everywhere; each subject gets its own strength and spatial mixing, on top of 1/f noise.
+    Trials are standardised per channel like the reference's exponential moving standardisation."""
+    sess = 0 if mode == "Train" else 1
+    rng = np.random.default_rng(1000 * subject + 17 * sess + 3)
+    srng = np.random.default_rng(1000 * subject)          # subject-specific, session-independent
+    y = np.repeat(np.arange(4), n // 4)
+    y = rng.permutation(np.concatenate([y, rng.integers(0, 4, n - y.size)]))
+    t = np.arange(T) / SFREQ
+    X = _pink_noise(rng, (n, C, T), T) * 1.5
+    mu_f = srng.uniform(9.0, 11.5)
+    beta_f = srng.uniform(19.0, 24.0)
+    strength = srng.uniform(0.6, 1.4)
+    mix = np.eye(C) + 0.15 * srng.standard_normal((C, C))
+    for i in range(n):
+        ph = rng.uniform(0, 2 * np.pi, 2)
+        rhythm = np.sin(2 * np.pi * mu_f * t + ph[0]) + 0.5 * np.sin(2 * np.pi * beta_f * t + ph[1])
+        amp = np.full(C, 1.0)
+        if y[i] == 0:
+            amp[C4] -= 0.8 * strength
+            amp[C3] += 0.3 * strength
+        elif y[i] == 1:
+            amp[C3] -= 0.8 * strength
+            amp[C4] += 0.3 * strength
+        elif y[i] == 2:
+            amp[CZ] -= 0.9 * strength
+        else:
+            amp *= 1.0 - 0.25 * strength
+        X[i] += mix @ (amp[:, None] * rhythm[None, :])
+    X = (X - X.mean(axis=2, keepdims=True)) / (X.std(axis=2, keepdims=True) + 1e-6)
+    return BCICI2ADataset(X.astype(np.float64), y.astype(np.int64))
+
+
+def data_dir() -> str:
+    return os.environ.get("EEGNET_DATA_DIR", os.path.join(os.getcwd(), "data", "processed"))
+
+
+def build_dataset_from_preprocessed(subject: int, mode: str = "Train") -> BCICI2ADataset:
+    """dataset.py:239-281 call signature.  Real epoched data from ``A0{s}{T|E}.npz`` if present
+    (X [288,22,257], y [288]), else the seeded synthetic session."""
+    tag = "T" if mode == "Train" else "E"
+    path = os.path.join(data_dir(), f"A0{subject}{tag}.npz")
+    if os.path.exists(path):
+        z = np.load(path, allow_pickle=False)
+        return BCICI2ADataset(np.asarray(z["X"], dtype=np.float64), np.asarray(z["y"], dtype=np.int64))
+    return synthetic_session(subject, mode)
+
+
+class DeviceLoader:
+    """``DataLoader(ds, batch_size, shuffle)`` with the split resident in HBM as fp32."""
+
+    def __init__(self, X, y, batch_size=64, shuffle=False, device="cuda", generator=None):
+        self.X = torch.as_tensor(np.asarray(X), dtype=torch.float32).to(device).contiguous()
+        self.y = torch.as_tensor(np.asarray(y), dtype=torch.int64).to(device)
+        self.batch_size = batch_size
+        self.shuffle = shuffle
+        self.generator = generator
+
+    def __len__(self):
+        return (len(self.y) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = len(self.y)
+        if self.shuffle:
+            idx = torch.randperm(n, generator=self.generator).to(self.X.device)
+            for s in range(0, n, self.batch_size):
+                j = idx[s:s + self.batch_size]
+                yield self.X.index_select(0, j), self.y.index_select(0, j)
+        else:
+            for s in range(0, n, self.batch_size):
+                yield self.X[s:s + self.batch_size], self.y[s:s + self.batch_size]

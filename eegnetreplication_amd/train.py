@@ -1,0 +1,283 @@
+"""Drop-in for the ``eegnet_repl.train`` CLI (PraKesEy/EEGNetReplication src/eegnet_repl/train.py).
+
+    python -m eegnetreplication_amd.train --trainingType Within-Subject --epochs 500
+    torchrun --nproc-per-node 8 -m eegnetreplication_amd.train --trainingType Cross-Subject
+
+Same protocols, hyper-parameters, checkpoint names and JSON report schema as the reference:
+
+* Within-Subject (train.py:30-148): per subject the Train+Eval sessions are concatenated, split by
+  ``KFold(4, shuffle=True, random_state=42)``; the first ``len(train_val)//5`` of each train_val
+  split is validation; EEGNet(p=0.5), Adam(lr=1e-3, eps=1e-7), CE, ``train()``; the best fold by
+  validation accuracy is saved as ``models/subject_XX_best_model.pth``.
+* Cross-Subject (train.py:151-291): 9 test subjects x 10 repeats = 90 folds; fold k draws
+  ``RandomState(42 + k).permutation(other subjects)`` -> 5 train / 3 val subjects; test on the
+  subject's Eval session; p=0.25; the fold with the lowest validation loss is saved as
+  ``models/cross_subject_best_model.pth``.
+
+MI355X specifics: the folds are independent units, dealt to ranks (one process per GPU) by
+``distributed.lpt_assign`` with no communication on the data path and merged on the host; every
+split lives in HBM (``DeviceLoader``); each unit is seeded (``--seed`` + unit index), which the
+reference does not do, so results do not depend on how units are sharded.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+from datetime import datetime
+
+import numpy as np
+import torch
+import torch.nn as nn
+from sklearn.model_selection import KFold
+
+from . import distributed as D
+from .dataset import BCICI2ADataset, DeviceLoader, build_dataset_from_preprocessed
+from .model import EEGNet, evaluate_model, train
+
+logger = logging.getLogger("eegnet_repl")
+
+BATCH_SIZE = 64
+EPOCHS = 500
+LEARNING_RATE = 0.001
+N_SUBJECTS = 9
+
+
+def _optimizer(model):
+    return torch.optim.Adam(model.parameters(), lr=LEARNING_RATE, eps=1e-07, foreach=None, fused=None)
+
+
+def _run_fold(X, y, tr_ids, va_ids, te, p, epochs, seed, device):
+    """One independent unit: build, train, evaluate.  Returns a picklable result dict."""
+    torch.manual_seed(seed)
+    gen = torch.Generator().manual_seed(seed)
+    tl = DeviceLoader(X[tr_ids], y[tr_ids], BATCH_SIZE, shuffle=True, device=device, generator=gen)
+    vl = DeviceLoader(X[va_ids], y[va_ids], BATCH_SIZE, shuffle=False, device=device)
+    tel = DeviceLoader(te[0], te[1], BATCH_SIZE, shuffle=False, device=device)
+    model = EEGNet(C=X.shape[1], T=X.shape[2], p=p)
+    opt = _optimizer(model)
+    best, _, val_losses, val_accs = train(model, opt, nn.CrossEntropyLoss(), tl, vl, nepochs=epochs)
+    model.load_state_dict(best)
+    test_acc = evaluate_model(model, tel)
+    return {"test_acc": test_acc, "val_acc": max(val_accs), "val_loss": min(val_losses),
+            "state": {k: v.detach().cpu() for k, v in best.items()}}
+
+
+def within_subject_units():
+    units = []
+    for s in range(1, N_SUBJECTS + 1):
+        for f in range(4):
+            units.append((s, f))
+    return units
+
+
+def within_subject_training(epochs=EPOCHS, seed=0, device="cuda"):
+    """train.py:30-148.  Returns (per_subject_test_acc, avg_test_acc, best_model_states)."""
+    rank, world, _ = D.env_rank_world()
+    units = within_subject_units()
+    mine = D.lpt_assign([1.0] * len(units), world)[rank] if world > 1 else range(len(units))
+    cache, local = {}, {}
+    for u in mine:
+        s, f = units[u]
+        if s not in cache:
+            tr = build_dataset_from_preprocessed(subject=s)
+            ev = build_dataset_from_preprocessed(subject=s, mode="Eval")
+            data = BCICI2ADataset(np.concatenate([tr.X, ev.X]), np.concatenate([tr.y, ev.y]))
+            splits = list(KFold(n_splits=4, shuffle=True, random_state=42).split(data.X))
+            cache[s] = (data, splits)
+        data, splits = cache[s]
+        train_val, test_ids = splits[f]
+        nval = len(train_val) // 5
+        logger.info(f"Subject {s} fold {f + 1}/4 on rank {rank}")
+        local[u] = _run_fold(data.X, data.y, train_val[nval:], train_val[:nval],
+                             (data.X[test_ids], data.y[test_ids]), 0.5, epochs, seed + u, device)
+    res = D.gather_results(local)
+    per_subject, states = [], []
+    for s in range(1, N_SUBJECTS + 1):
+        accs, best_val, best_state = [], 0, None
+        for f in range(4):
+            r = res[units.index((s, f))]
+            logger.info(f"Subject {s} fold {f + 1}: val {r['val_acc']:.2f}% test {r['test_acc']:.2f}%")
+            accs.append(r["test_acc"])
+            if r["val_acc"] > best_val:
+                best_val, best_state = r["val_acc"], r["state"]
+        per_subject.append(sum(accs) / len(accs))
+        states.append(best_state)
+    avg = sum(per_subject) / len(per_subject)
+    logger.info(f"Overall Average Test Accuracy across all subjects: {avg:.2f}%")
+    return per_subject, avg, states
+
+
+def cross_subject_units():
+    units, k = [], 0
+    for s in range(1, N_SUBJECTS + 1):
+        others = [o for o in range(1, N_SUBJECTS + 1) if o != s]
+        for _ in range(10):
+            k += 1
+            perm = np.random.RandomState(42 + k).permutation(others)
+            units.append((s, k, [int(v) for v in perm[:5]], [int(v) for v in perm[5:]]))
+    return units
+
+
+def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda"):
+    """train.py:151-291.  Returns (best_model_state, per_subject_test_acc, avg_test_acc)."""
+    rank, world, _ = D.env_rank_world()
+    units = cross_subject_units()
+    mine = D.lpt_assign([1.0] * len(units), world)[rank] if world > 1 else range(len(units))
+    sessions = {}
+
+    def sess(s, mode):
+        if (s, mode) not in sessions:
+            sessions[(s, mode)] = build_dataset_from_preprocessed(subject=s, mode=mode)
+        return sessions[(s, mode)]
+
+    local = {}
+    for u in mine:
+        s, k, trs, vas = units[u]
+        X = np.concatenate([sess(v, "Train").X for v in trs + vas])
+        y = np.concatenate([sess(v, "Train").y for v in trs + vas])
+        ntr = sum(len(sess(v, "Train").y) for v in trs)
+        ids = np.arange(len(y))
+        te = sess(s, "Eval")
+        logger.info(f"Fold {k}/90 (Subject {s}) on rank {rank}")
+        local[u] = _run_fold(X, y, ids[:ntr], ids[ntr:], (te.X, te.y), 0.25, epochs, seed + u, device)
+    res = D.gather_results(local)
+    per_subject, all_acc = [], []
+    best_loss, best_state = 100, None
+    for s in range(1, N_SUBJECTS + 1):
+        accs = []
+        for u, unit in enumerate(units):
+            if unit[0] != s:
+                continue
+            r = res[u]
+            accs.append(r["test_acc"])
+            all_acc.append(r["test_acc"])
+            if r["val_loss"] < best_loss:
+                best_loss, best_state = r["val_loss"], r["state"]
+        per_subject.append(sum(accs) / len(accs))
+    avg = sum(all_acc) / len(all_acc)
+    se = float(np.std(all_acc) / np.sqrt(len(all_acc)))
+    logger.info(f"Overall Average Test Accuracy: {avg:.2f}% +- {se:.2f}%")
+    return best_state, per_subject, avg
+
+
+def _ranked(per_subject, key):
+    rows = [{key: i + 1, "test_accuracy": round(a, 2), "performance_rank": 0}
+            for i, a in enumerate(per_subject)]
+    for rank, r in enumerate(sorted(rows, key=lambda r: r["test_accuracy"], reverse=True), 1):
+        r["performance_rank"] = rank
+    return rows
+
+
+def _summary(per_subject, avg):
+    return {
+        "accuracy_distribution": {
+            "above_average_subjects": sum(a > avg for a in per_subject),
+            "below_average_subjects": sum(a < avg for a in per_subject),
+            "at_average_subjects": sum(a == avg for a in per_subject)},
+        "accuracy_quartiles": {
+            "q1": round(float(np.percentile(per_subject, 25)), 2),
+            "q2_median": round(float(np.percentile(per_subject, 50)), 2),
+            "q3": round(float(np.percentile(per_subject, 75)), 2)},
+    }
+
+
+def _write_report(report, prefix, out_dir):
+    os.makedirs(out_dir, exist_ok=True)
+    stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
+    path = os.path.join(out_dir, f"{prefix}_training_report_{stamp}.json")
+    for p in (path, os.path.join(out_dir, f"latest_{prefix}_report.json")):
+        with open(p, "w", encoding="utf-8") as f:
+            json.dump(report, f, indent=2, ensure_ascii=False)
+    logger.info(f"report written to {path}")
+    return path
+
+
+def generate_ws_report(per_subject_test_acc, avg, states, out_dir="reports"):
+    """JSON schema of train.py:309-368."""
+    rows = _ranked(per_subject_test_acc, "subject_id")
+    for r in rows:
+        r["model_saved"] = f"subject_{r['subject_id']:02d}_best_model.pth"
+        r["performance_rank"] = r.pop("performance_rank")
+    report = {
+        "training_type": "Within-Subject",
+        "timestamp": datetime.now().isoformat(),
+        "model_parameters": {"batch_size": BATCH_SIZE, "epochs": EPOCHS, "learning_rate": LEARNING_RATE,
+                             "dropout_probability": 0.5, "cross_validation_folds": 4},
+        "overall_results": {"average_test_accuracy": round(avg, 2),
+                            "number_of_subjects": len(per_subject_test_acc),
+                            "best_subject_accuracy": round(max(per_subject_test_acc), 2),
+                            "worst_subject_accuracy": round(min(per_subject_test_acc), 2),
+                            "accuracy_std": round(float(np.std(per_subject_test_acc)), 2)},
+        "per_subject_results": rows,
+        "model_info": {"architecture": "EEGNet", "optimizer": "Adam",
+                       "loss_function": "CrossEntropyLoss", "saved_models_count": len(states)},
+        "summary_statistics": _summary(per_subject_test_acc, avg),
+    }
+    return _write_report(report, "within_subject", out_dir)
+
+
+def generate_cs_report(best_state, per_subject_test_acc, avg, out_dir="reports"):
+    """JSON schema of train.py:406-468 (standard_error over per-subject means, as the reference)."""
+    report = {
+        "training_type": "Cross-Subject",
+        "timestamp": datetime.now().isoformat(),
+        "model_parameters": {"batch_size": BATCH_SIZE, "epochs": EPOCHS, "learning_rate": LEARNING_RATE,
+                             "dropout_probability": 0.25, "total_folds": 90, "repeats_per_subject": 10,
+                             "train_subjects_per_fold": 5, "validation_subjects_per_fold": 3},
+        "overall_results": {
+            "average_test_accuracy": round(avg, 2),
+            "standard_error": round(float(np.std(per_subject_test_acc) / np.sqrt(len(per_subject_test_acc))), 2),
+            "number_of_test_subjects": len(per_subject_test_acc),
+            "best_subject_accuracy": round(max(per_subject_test_acc), 2),
+            "worst_subject_accuracy": round(min(per_subject_test_acc), 2),
+            "accuracy_std": round(float(np.std(per_subject_test_acc)), 2)},
+        "per_subject_results": _ranked(per_subject_test_acc, "test_subject_id"),
+        "model_info": {"architecture": "EEGNet", "optimizer": "Adam",
+                       "loss_function": "CrossEntropyLoss", "saved_model": "cross_subject_best_model.pth"},
+        "summary_statistics": _summary(per_subject_test_acc, avg),
+    }
+    return _write_report(report, "cross_subject", out_dir)
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser(description="Train a EEGNet model (MI355X).")
+    ap.add_argument("--trainingType", type=str, default="Within-Subject",
+                    help="Training type [Cross-Subject, Within-Subject].")
+    ap.add_argument("--epochs", type=int, default=EPOCHS, help="Number of training epochs.")
+    ap.add_argument("--generateReport", type=bool, default=True, help="Generate report after training.")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", type=str, default=".", help="directory for models/ and reports/")
+    args = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO,
+                        format="%(asctime)s - %(filename)s - %(funcName)s - %(levelname)s - %(message)s",
+                        handlers=[logging.FileHandler("app.log"), logging.StreamHandler()])
+    rank, world, local = D.init_process_group()
+    device = f"cuda:{local}"
+    torch.cuda.set_device(local)
+    models_dir = os.path.join(args.out, "models")
+    reports_dir = os.path.join(args.out, "reports")
+    if args.trainingType == "Within-Subject":
+        per_subject, avg, states = within_subject_training(args.epochs, args.seed, device)
+        if rank == 0:
+            os.makedirs(models_dir, exist_ok=True)
+            for s, st in enumerate(states, 1):
+                torch.save(st, os.path.join(models_dir, f"subject_{s:02d}_best_model.pth"))
+            if args.generateReport:
+                generate_ws_report(per_subject, avg, states, reports_dir)
+    else:
+        best, per_subject, avg = cross_subject_training(args.epochs, args.seed, device)
+        if rank == 0:
+            os.makedirs(models_dir, exist_ok=True)
+            torch.save(best, os.path.join(models_dir, "cross_subject_best_model.pth"))
+            if args.generateReport:
+                generate_cs_report(best, per_subject, avg, reports_dir)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
