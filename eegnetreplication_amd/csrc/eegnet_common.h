@@ -21,6 +21,15 @@ constexpr int F2MAX = 16;     // rows per trial plane this build keeps one-per-w
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// 16-byte LDS accesses as one <4 x float> with alignment 16 (ds_read_b128 / ds_write_b128); a HIP
+// float4 struct access gets scalarised into lane-strided ds_read_b32, a 4-way bank conflict
+__device__ __forceinline__ floatx4 lds_ld4(const float* p) {
+    return *reinterpret_cast<const floatx4*>(__builtin_assume_aligned(p, 16));
+}
+__device__ __forceinline__ void lds_st4(float* p, floatx4 v) {
+    *reinterpret_cast<floatx4*>(__builtin_assume_aligned(p, 16)) = v;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Geometry shared by host and device (passed by value).  All LDS carve sizes come from the host.
 // ------------------------------------------------------------------------------------------------
@@ -117,11 +126,10 @@ __device__ __forceinline__ void wave_lds_fence() {
 // NW aligned float4 loads from LDS (p must be 16-byte aligned: row base + multiple of 4 floats)
 template <int NW>
 __device__ __forceinline__ void lds_window(const float* __restrict__ p, float (&w)[4 * NW]) {
-    const float4* p4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(p, 16));
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
-        const float4 f = p4[i];
-        w[4 * i + 0] = f.x; w[4 * i + 1] = f.y; w[4 * i + 2] = f.z; w[4 * i + 3] = f.w;
+        const floatx4 f = lds_ld4(p + 4 * i);
+        w[4 * i + 0] = f[0]; w[4 * i + 1] = f[1]; w[4 * i + 2] = f[2]; w[4 * i + 3] = f[3];
     }
 }
 
@@ -170,8 +178,7 @@ __device__ __forceinline__ void x_store(const float (&pf)[PF], int C, int T, int
             const int i = tid + NTH * j;
             if (4 * i < n) {
                 const int c = i / TQ, q = i - c * TQ;
-                *reinterpret_cast<float4*>(Xs + c * RS + LP + 4 * q) =
-                    make_float4(pf[4 * j], pf[4 * j + 1], pf[4 * j + 2], pf[4 * j + 3]);
+                lds_st4(Xs + c * RS + LP + 4 * q, (floatx4){pf[4 * j], pf[4 * j + 1], pf[4 * j + 2], pf[4 * j + 3]});
             }
         }
     } else {

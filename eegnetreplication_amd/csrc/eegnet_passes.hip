@@ -721,7 +721,7 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* __restrict__
                     for (int i = 0; i < 4; ++i) a = fmaf(dy[i], w[G_::OFF + i + k], a);
                     Q[k] = a;
                 }
-                *reinterpret_cast<float4*>(drow + 4 * q) = make_float4(dy[0], dy[1], dy[2], dy[3]);
+                lds_st4(drow + 4 * q, (floatx4){dy[0], dy[1], dy[2], dy[3]});
             }
             wave_lds_fence();
             // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
@@ -738,7 +738,7 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* __restrict__
                     for (int m = 0; m < K1; ++m) a = fmaf(tap[K1 - 1 - m], w[G_::OFFD + i + m], a);
                     e[i] = (4 * q + i < T) ? a : 0.f;
                 }
-                *reinterpret_cast<float4*>(erow + 4 * q) = make_float4(e[0], e[1], e[2], e[3]);
+                lds_st4(erow + 4 * q, (floatx4){e[0], e[1], e[2], e[3]});
             }
         }
         if (xdb && bn < g.B) x_store<PF>(pf, C, T, RS, LP, Xn, tid);
@@ -751,14 +751,14 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* __restrict__
             const float* brow = Xc + (c < C ? c : 0) * RS + LP + 4 * lk;
             const bool aon = li < F2, bon = c < C;
             for (int kg = kg0; kg < kg1; ++kg) {
-                float4 a4 = *reinterpret_cast<const float4*>(arow + 16 * kg);
-                float4 b4 = *reinterpret_cast<const float4*>(brow + 16 * kg);
-                if (!aon) a4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (!bon) b4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, xacc, 0, 0, 0);
+                floatx4 a4 = lds_ld4(arow + 16 * kg);
+                floatx4 b4 = lds_ld4(brow + 16 * kg);
+                if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
             }
         }
         __syncthreads();                                   // e rows consumed before the next s
