@@ -51,6 +51,7 @@ struct Geo {
     // partial-row lengths of the five passes and the (common) workgroup count
     int nA, nB, nC, nD, nE;
     int grid;
+    int rgs, ngrp;       // in-kernel reduction: partial rows per group, groups (<= NGRPMAX)
     // LDS (floats)
     int ldsA, ldsB, ldsC, ldsD, ldsE, ldsI;
 };
@@ -63,6 +64,28 @@ enum CoefField {
 constexpr int CSTR = 64;
 
 enum PassCMode { PC_LOGITS = 1, PC_BWD = 2, PC_CE = 4 };
+
+// In-kernel reduction + finalize (eegnet_finalize.hip): every pass kernel ends with a ticketed
+// two-level fp64 reduction of its per-workgroup partial rows; the last workgroup to arrive runs that
+// pass's finalize.  Ticket words: NCNT per pass, zeroed by a memset node at the start of every call.
+constexpr int NGRPMAX = 15;
+constexpr int NCNT = 16;          // [0, ngrp) group tickets, [NCNT-1] the top-level ticket
+struct FinArgs {
+    double* part2;                // [ngrp][ncols] fp64 group partials
+    unsigned* cnt;                // this pass's NCNT ticket words
+    double* stats;                // lag-Gram + window sums (fin1 writes, fin5 reads)
+    float* coef;
+    float* bn;                    // running statistics (fin1/fin2, when update_running)
+    float* grads;
+    float* loss;
+    int update_running, ce;
+    // Adam (torch.optim.Adam) fused into pass E's finalize when adam_m != nullptr
+    float* params;
+    float* adam_m;
+    float* adam_v;
+    int32_t* step;
+    float lr, b1, b2, eps;
+};
 
 // padded-row strides, shared by host (make_geo) and the compile-time-shape kernels
 __host__ __device__ constexpr int rup4(int a) { return (a + 3) & ~3; }

@@ -1,43 +1,104 @@
-// eegnet_finalize.hip -- deterministic fp64 reductions, the one-workgroup finalize kernels (BN
-// constants, running statistics, parameter gradients, clamps) and the Adam update.
+// eegnet_finalize.hip -- the in-kernel deterministic fp64 reduction that ends every pass, the finalize
+// bodies its last workgroup runs (BN constants, running statistics, parameter gradients, clamps, Adam)
+// and the standalone Adam / clamp kernels of the data-parallel path.
 // Included by eegnet_kernels.hip (one translation unit).
 
 namespace eeg {
 
 // ================================================================================================
-// Deterministic fp64 column reduction of per-workgroup partial rows, stage 1: the rows are cut into
-// RCH chunks; workgroup (column block, chunk) writes one fp64 partial per column.  Stage 2 (the
-// RCH-way sum per column) is the prologue of the finalize kernel that consumes the sums.
+// In-kernel deterministic fp64 reduction of the per-workgroup partial rows (cdna_hip_programming.md
+// §6 Guideline 16, counter form).  Every workgroup of a pass publishes its row (write-through stores,
+// every wave drains, barrier, one lane: relaxed agent ticket add).  The last arriver of
+// each group of g.rgs rows sums the group's rows in fp64 (agent acquire first) into part2; the last
+// of those group reducers sums the g.ngrp group partials into S (LDS) and runs the pass's finalize.
+// The summation order is fixed by (row, column) alone, so results do not depend on arrival order.
 // ================================================================================================
-constexpr int RCH = 32;
 
-__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ part, int nrows, int ncols,
-                                               double* __restrict__ part2) {
-    __shared__ double red[4][64];
-    const int tid = threadIdx.x, col = blockIdx.x * 64 + (tid & 63), rg = tid >> 6;
-    const int r0 = (nrows * (int)blockIdx.y) / RCH, r1 = (nrows * ((int)blockIdx.y + 1)) / RCH;
-    double a = 0.0;
-    if (col < ncols)
-        for (int r = r0 + rg; r < r1; r += 4) a += (double)part[(size_t)r * ncols + col];
-    red[rg][tid & 63] = a;
-    __syncthreads();
-    if (tid < 64 && col < ncols)
-        part2[(size_t)blockIdx.y * ncols + col] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+// Partial rows and group partials are published write-through (sc1 stores, Guideline 16 R1), so no
+// agent release fence is needed: each storing wave drains its stores before the workgroup barrier,
+// then one lane adds the ticket.  The ticket winner's agent acquire drops this CU's stale L1 lines
+// before its plain loads.
+__device__ __forceinline__ void pub(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pub(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// stage 2, run by the one finalize workgroup: S[c] = sum over the RCH chunk partials
-__device__ __forceinline__ void reduce_chunks(const double* __restrict__ part2, int ncols, double* S) {
-    for (int c = threadIdx.x; c < ncols; c += 256) {
-        double a = 0.0;
-#pragma unroll 8
-        for (int r = 0; r < RCH; ++r) a += part2[(size_t)r * ncols + c];
-        S[c] = a;
+// all threads call; returns (workgroup-uniformly) whether this workgroup took the last of `target`
+// tickets on *w.  `flag` is one LDS word nobody else touches between the two barriers.
+__device__ __forceinline__ bool take_ticket(unsigned* w, unsigned target, int* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == target - 1u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
     }
     __syncthreads();
+    return *flag != 0;
+}
+
+// LDS carve-up of the tail (doubles, from the start of the pass kernel's dynamic LDS, which is no
+// longer in use once the partial row is written): [flag 2][S rup2(ncols)][scratch]
+__host__ __device__ constexpr int tail_scratch_doubles(int ncols) { return ncols > NTH ? ncols : NTH; }
+__host__ __device__ constexpr int tail_s_doubles(int ncols) { return 2 + ((ncols + 1) & ~1); }
+
+__device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const FinArgs& fa, double* dsm) {
+    const int tid = threadIdx.x;
+    int* flag = (int*)dsm;
+    double* S = dsm + 2;
+    double* scr = dsm + tail_s_doubles(ncols);
+    const int grp = blockIdx.x / g.rgs;
+    const int r0 = grp * g.rgs, r1 = min(g.grid, r0 + g.rgs), nr = r1 - r0;
+    if (!take_ticket(fa.cnt + grp, (unsigned)nr, flag)) return false;
+    // group reducer: rows [r0, r1), rs interleaved row subsets per column, then the rs-way sum
+    const int rs = max(1, min(nr, NTH / ncols));
+    for (int idx = tid; idx < rs * ncols; idx += NTH) {
+        const int sub = idx / ncols, c = idx - sub * ncols;
+        const float* col = part + c;
+        double a = 0.0;
+        int r = r0 + sub;
+        for (; r + 7 * rs < r1; r += 8 * rs) {      // 8 loads in flight, summed in row order
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = col[(size_t)(r + j * rs) * ncols];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a += (double)v[j];
+        }
+        for (; r < r1; r += rs) a += (double)col[(size_t)r * ncols];
+        scr[idx] = a;
+    }
+    __syncthreads();
+    for (int c = tid; c < ncols; c += NTH) {
+        double a = 0.0;
+        for (int sub = 0; sub < rs; ++sub) a += scr[sub * ncols + c];
+        pub(fa.part2 + (size_t)grp * ncols + c, a);
+    }
+    if (!take_ticket(fa.cnt + (NCNT - 1), (unsigned)g.ngrp, flag)) return false;
+    for (int c = tid; c < ncols; c += NTH) {
+        double v[NGRPMAX];
+#pragma unroll
+        for (int q = 0; q < NGRPMAX; ++q) v[q] = q < g.ngrp ? fa.part2[(size_t)q * ncols + c] : 0.0;
+        double a = 0.0;
+#pragma unroll
+        for (int q = 0; q < NGRPMAX; ++q) if (q < g.ngrp) a += v[q];
+        S[c] = a;
+    }
+    // every ticket of this pass has been taken: re-arm them (the per-call memset is the guarantee)
+    if (tid < g.ngrp) __hip_atomic_store(fa.cnt + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(fa.cnt + (NCNT - 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return true;
 }
 
 // ================================================================================================
-// Finalize kernels (one workgroup each): BN constants, running statistics, parameter gradients.
+// Finalize bodies (run by the last workgroup of each pass, NTH threads): BN constants, running
+// statistics, parameter gradients, clamps; Adam after pass E.
 // ================================================================================================
 __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, double var, double n,
                                            float mom) {
@@ -45,20 +106,20 @@ __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, doub
     *rv = (float)((1.0 - mom) * (double)*rv + mom * var * n / (n - 1.0));
 }
 
+__host__ __device__ constexpr int fin1_scratch_doubles(int K1, int F1) { return K1 * K1 + K1 + 128 + 3 * F1 * K1; }
+__host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1) { return K1 * K1 + K1 + 128 + F1 * K1; }
+
 // after pass A: BN1 (model.py:32) and BN2 (model.py:47) batch statistics
-__global__ __launch_bounds__(256) void k_fin1(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ part2,
-                                             double* __restrict__ stats, float* __restrict__ coef,
-                                             float* __restrict__ bn, int update_running) {
-    extern __shared__ __attribute__((aligned(16))) double dsm[];
-    const int K1 = g.K1;
-    double* Gm = dsm;                 // K1*K1
+__device__ void fin1(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
+    const int K1 = g.K1, F1 = g.F1;
+    double* Gm = scr;                 // K1*K1
     double* S1 = Gm + K1 * K1;        // K1
-    double* a1s = S1 + K1;            // F1
+    double* a1s = S1 + K1;            // F1 (<= 64)
     double* c1s = a1s + 64;
-    double* sums = c1s + 64;          // nA
+    double* wd = c1s + 64;            // F1*K1 temporal taps
+    double* pq = wd + F1 * K1;        // F1*K1 w[k] (G w)[k]
+    double* pm = pq + F1 * K1;        // F1*K1 w[k] S1[k]
     const int tid = threadIdx.x;
-    reduce_chunks(part2, g.nA, sums);
     const double* G0 = sums;
     const double S0 = sums[K1];
     const double* H = sums + K1 + 1;                 // head pairs (a <= b < R), a-major
@@ -87,36 +148,41 @@ __global__ __launch_bounds__(256) void k_fin1(Geo g, const float* __restrict__ p
             }
         }
     }
-    if (tid == 0) {      // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j])
+    if (tid == 64) {      // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j])
         double acc = S0;
         for (int k = 0; k < K1; ++k) {
             S1[k] = acc;
             if (k < K1 - 1) acc += (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
         }
     }
+    for (int i = tid; i < F1 * K1; i += NTH) wd[i] = (double)prm[g.o_w1 + i];
     __syncthreads();
-    for (int i = tid; i < K1 * K1 + K1; i += 256) stats[i] = Gm[i];
+    for (int i = tid; i < K1 * K1 + K1; i += NTH) fa.stats[i] = Gm[i];
+    // quadratic forms w^T G w and w^T S1, one (filter, tap) per thread (G symmetric: column reads)
+    for (int p = tid; p < F1 * K1; p += NTH) {
+        const int gg = p / K1, k = p - gg * K1;
+        const double* w = wd + gg * K1;
+        double r = 0.0;
+        for (int l = 0; l < K1; ++l) r += Gm[l * K1 + k] * w[l];
+        pq[p] = w[k] * r;
+        pm[p] = w[k] * S1[k];
+    }
+    __syncthreads();
     const double n1 = (double)g.B * g.C * g.T;
-    if (tid < g.F1) {
-        const float* w = prm + g.o_w1 + tid * K1;
+    if (tid < F1) {
         double mu = 0.0, e2 = 0.0;
-        for (int k = 0; k < K1; ++k) {
-            mu += (double)w[k] * S1[k];
-            double r = 0.0;
-            for (int l = 0; l < K1; ++l) r += Gm[k * K1 + l] * (double)w[l];
-            e2 += (double)w[k] * r;
-        }
+        for (int k = 0; k < K1; ++k) { mu += pm[tid * K1 + k]; e2 += pq[tid * K1 + k]; }
         mu /= n1;
         const double var = e2 / n1 - mu * mu;
         const double inv = 1.0 / sqrt(var + (double)g.eps);
         const double a1 = (double)prm[g.o_g1 + tid] * inv;
         const double c1 = (double)prm[g.o_b1 + tid] - a1 * mu;
         a1s[tid] = a1; c1s[tid] = c1;
-        coef[CF_A1 * CSTR + tid] = (float)a1;
-        coef[CF_C1 * CSTR + tid] = (float)c1;
-        coef[CF_INV1 * CSTR + tid] = (float)inv;
-        coef[CF_MU1 * CSTR + tid] = (float)mu;
-        if (update_running) bn_running(bn + tid, bn + g.F1 + tid, mu, var, n1, g.mom);
+        fa.coef[CF_A1 * CSTR + tid] = (float)a1;
+        fa.coef[CF_C1 * CSTR + tid] = (float)c1;
+        fa.coef[CF_INV1 * CSTR + tid] = (float)inv;
+        fa.coef[CF_MU1 * CSTR + tid] = (float)mu;
+        if (fa.update_running) bn_running(fa.bn + tid, fa.bn + F1 + tid, mu, var, n1, g.mom);
     }
     __syncthreads();
     const double n2 = (double)g.B * g.T;
@@ -130,136 +196,142 @@ __global__ __launch_bounds__(256) void k_fin1(Geo g, const float* __restrict__ p
         const double var2 = a1s[gg] * a1s[gg] * varv;
         const double inv2 = 1.0 / sqrt(var2 + (double)g.eps);
         const double alpha = a1s[gg] * inv2;
-        coef[CF_AL2 * CSTR + o] = (float)alpha;
-        coef[CF_BE2 * CSTR + o] = (float)(-alpha * mv);
-        coef[CF_INV2 * CSTR + o] = (float)inv2;
-        coef[CF_W * CSTR + o] = (float)W;
-        float* rm2 = bn + 2 * g.F1;
-        if (update_running) bn_running(rm2 + o, rm2 + g.F2 + o, mu2, var2, n2, g.mom);
+        fa.coef[CF_AL2 * CSTR + o] = (float)alpha;
+        fa.coef[CF_BE2 * CSTR + o] = (float)(-alpha * mv);
+        fa.coef[CF_INV2 * CSTR + o] = (float)inv2;
+        fa.coef[CF_W * CSTR + o] = (float)W;
+        float* rm2 = fa.bn + 2 * F1;
+        if (fa.update_running) bn_running(rm2 + o, rm2 + g.F2 + o, mu2, var2, n2, g.mom);
     }
 }
 
 // after pass B: BN3 (model.py:71) batch statistics
-__global__ __launch_bounds__(256) void k_fin2(Geo g, const double* __restrict__ part2,
-                                             float* __restrict__ coef, float* __restrict__ bn,
-                                             int update_running) {
-    extern __shared__ __attribute__((aligned(16))) double sums[];
-    reduce_chunks(part2, g.nB, sums);
+__device__ void fin2(const Geo& g, const double* sums, const FinArgs& fa) {
     const int j = threadIdx.x;
     if (j >= g.F2) return;
     const double n3 = (double)g.B * g.T1;
     const double mu = sums[j] / n3;
     const double var = sums[g.F2 + j] / n3 - mu * mu;
-    coef[CF_MU3 * CSTR + j] = (float)mu;
-    coef[CF_INV3 * CSTR + j] = (float)(1.0 / sqrt(var + (double)g.eps));
-    float* rm3 = bn + 2 * g.F1 + 2 * g.F2;
-    if (update_running) bn_running(rm3 + j, rm3 + g.F2 + j, mu, var, n3, g.mom);
+    fa.coef[CF_MU3 * CSTR + j] = (float)mu;
+    fa.coef[CF_INV3 * CSTR + j] = (float)(1.0 / sqrt(var + (double)g.eps));
+    float* rm3 = fa.bn + 2 * g.F1 + 2 * g.F2;
+    if (fa.update_running) bn_running(rm3 + j, rm3 + g.F2 + j, mu, var, n3, g.mom);
 }
 
 // after pass C: classifier grads (+ clamp, model.py:84), BN3 grads and backward constants
-__global__ __launch_bounds__(256) void k_fin3(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ part2,
-                                             float* __restrict__ coef, float* __restrict__ grads,
-                                             float* __restrict__ loss, int ce) {
-    extern __shared__ __attribute__((aligned(16))) double sums[];
-    reduce_chunks(part2, g.nC, sums);
+__device__ void fin3(const Geo& g, const float* prm, const double* sums, const FinArgs& fa) {
     const int tid = threadIdx.x;
     const int n4 = NCLS * g.NF;
-    for (int p = tid; p < n4; p += 256) {
+    for (int p = tid; p < n4; p += NTH) {
         const float v = (float)sums[p];
-        grads[g.o_Wfc + p] = g.noclamp ? v : fminf(fmaxf(v, -0.25f), 0.25f);
+        fa.grads[g.o_Wfc + p] = g.noclamp ? v : fminf(fmaxf(v, -0.25f), 0.25f);
     }
-    if (tid < NCLS) grads[g.o_bfc + tid] = (float)sums[n4 + tid];
+    if (tid < NCLS) fa.grads[g.o_bfc + tid] = (float)sums[n4 + tid];
     if (tid < g.F2) {
         const int j = tid;
         const double sdz = sums[n4 + NCLS + j], sdzx = sums[n4 + NCLS + g.F2 + j];
-        grads[g.o_b3 + j] = (float)sdz;
-        grads[g.o_g3 + j] = (float)sdzx;
+        fa.grads[g.o_b3 + j] = (float)sdz;
+        fa.grads[g.o_g3 + j] = (float)sdzx;
         const double n3 = (double)g.B * g.T1;
-        const double A = (double)prm[g.o_g3 + j] * (double)coef[CF_INV3 * CSTR + j];
-        coef[CF_A3 * CSTR + j] = (float)A;
-        coef[CF_B3 * CSTR + j] = (float)(-A * sdz / n3);
-        coef[CF_C3 * CSTR + j] = (float)(-A * sdzx / n3);
+        const double A = (double)prm[g.o_g3 + j] * (double)fa.coef[CF_INV3 * CSTR + j];
+        fa.coef[CF_A3 * CSTR + j] = (float)A;
+        fa.coef[CF_B3 * CSTR + j] = (float)(-A * sdz / n3);
+        fa.coef[CF_C3 * CSTR + j] = (float)(-A * sdzx / n3);
     }
-    if (tid == 0 && ce) {
+    if (tid == 0 && fa.ce) {
         const float l = (float)(sums[n4 + NCLS + 2 * g.F2] / (double)g.B);
-        coef[CF_LOSS * CSTR] = l;
-        if (loss) *loss = l;
+        fa.coef[CF_LOSS * CSTR] = l;
+        if (fa.loss) *fa.loss = l;
     }
 }
 
 // after pass D: block_2 grads, BN2 grads and the dy2 constants
-__global__ __launch_bounds__(256) void k_fin4(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ part2,
-                                             float* __restrict__ coef, float* __restrict__ grads) {
-    extern __shared__ __attribute__((aligned(16))) double sums[];
-    reduce_chunks(part2, g.nD, sums);
+__device__ void fin4(const Geo& g, const float* prm, const double* sums, const FinArgs& fa) {
     const int tid = threadIdx.x;
-    for (int p = tid; p < g.F2 * g.F2; p += 256) grads[g.o_W3 + p] = (float)sums[p];
-    for (int p = tid; p < g.F2 * 16; p += 256) grads[g.o_w2 + p] = (float)sums[g.F2 * g.F2 + p];
+    for (int p = tid; p < g.F2 * g.F2; p += NTH) fa.grads[g.o_W3 + p] = (float)sums[p];
+    for (int p = tid; p < g.F2 * 16; p += NTH) fa.grads[g.o_w2 + p] = (float)sums[g.F2 * g.F2 + p];
     if (tid < g.F2) {
         const int o = tid;
         const double sdz = sums[g.F2 * g.F2 + 16 * g.F2 + o];
         const double sdzx = sums[g.F2 * g.F2 + 17 * g.F2 + o];
-        grads[g.o_b2 + o] = (float)sdz;
-        grads[g.o_g2 + o] = (float)sdzx;
+        fa.grads[g.o_b2 + o] = (float)sdz;
+        fa.grads[g.o_g2 + o] = (float)sdzx;
         const double n2 = (double)g.B * g.T;
-        const double A = (double)prm[g.o_g2 + o] * (double)coef[CF_INV2 * CSTR + o];
-        coef[CF_AO * CSTR + o] = (float)A;
-        coef[CF_BO * CSTR + o] = (float)(-A * sdz / n2);
-        coef[CF_CO * CSTR + o] = (float)(-A * sdzx / n2);
+        const double A = (double)prm[g.o_g2 + o] * (double)fa.coef[CF_INV2 * CSTR + o];
+        fa.coef[CF_AO * CSTR + o] = (float)A;
+        fa.coef[CF_BO * CSTR + o] = (float)(-A * sdz / n2);
+        fa.coef[CF_CO * CSTR + o] = (float)(-A * sdzx / n2);
     }
 }
 
-// after pass E: spatial grad (+ clamp, model.py:44), BN1 grads, temporal-conv grad
-__global__ __launch_bounds__(256) void k_fin5(Geo g, const float* __restrict__ prm,
-                                             const double* __restrict__ part2,
-                                             const double* __restrict__ stats,
-                                             const float* __restrict__ coef,
-                                             float* __restrict__ grads) {
-    extern __shared__ __attribute__((aligned(16))) double sums[];
-    reduce_chunks(part2, g.nE, sums);
-    __shared__ double db1s[64], dg1s[64];
-    const int tid = threadIdx.x, K1 = g.K1;
+// one torch.optim.Adam element update (weight_decay=0, amsgrad=False): torch/optim/adam.py
+// :457,476,531-547 (single-tensor path)
+__device__ __forceinline__ void adam_elem(float* p, float g, float* m, float* v, float b1, float b2,
+                                          float step_size, float bc2s, float eps) {
+    const float mi = *m + (1.f - b1) * (g - *m);
+    const float vi = b2 * *v + (1.f - b2) * g * g;
+    *m = mi; *v = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    *p = *p - step_size * (mi / denom);
+}
+
+// after pass E: spatial grad (+ clamp, model.py:44), BN1 grads, temporal-conv grad; then Adam
+__device__ void fin5(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
+    const int tid = threadIdx.x, K1 = g.K1, F1 = g.F1;
+    double* Gm = scr;                 // K1*K1 (+ S1 K1), copied from fa.stats
+    double* S1 = Gm + K1 * K1;
+    double* db1s = S1 + K1;           // 64
+    double* dg1s = db1s + 64;         // 64
+    double* wd = dg1s + 64;           // F1*K1
     const double* Q = sums;
     const double* Xm = sums + g.F2 * K1;
     const double* Sdy = Xm + g.F2 * g.C;
     const double* Sdyv = Sdy + g.F2;
-    const double* Gm = stats;
-    const double* S1 = stats + K1 * K1;
-    for (int p = tid; p < g.F2 * g.C; p += 256) {
+    for (int i = tid; i < K1 * K1 + K1; i += NTH) Gm[i] = fa.stats[i];
+    for (int i = tid; i < F1 * K1; i += NTH) wd[i] = (double)prm[g.o_w1 + i];
+    for (int p = tid; p < g.F2 * g.C; p += NTH) {
         const int o = p / g.C, gg = o / g.D;
-        const double v = (double)coef[CF_A1 * CSTR + gg] * Xm[p] + (double)coef[CF_C1 * CSTR + gg] * Sdy[o];
-        grads[g.o_ws + p] = g.noclamp ? (float)v : fminf(fmaxf((float)v, -1.0f), 1.0f);
+        const double v = (double)fa.coef[CF_A1 * CSTR + gg] * Xm[p] + (double)fa.coef[CF_C1 * CSTR + gg] * Sdy[o];
+        fa.grads[g.o_ws + p] = g.noclamp ? (float)v : fminf(fmaxf((float)v, -1.0f), 1.0f);
     }
-    const double n1 = (double)g.B * g.C * g.T;
-    if (tid < g.F1) {
+    if (tid < F1) {
         const int gg = tid;
         double db1 = 0.0, dyu = 0.0;
         for (int o = gg * g.D; o < (gg + 1) * g.D; ++o) {
-            db1 += (double)coef[CF_W * CSTR + o] * Sdy[o];
+            db1 += (double)fa.coef[CF_W * CSTR + o] * Sdy[o];
             dyu += Sdyv[o];
         }
-        const double inv1 = coef[CF_INV1 * CSTR + gg], mu1 = coef[CF_MU1 * CSTR + gg];
+        const double inv1 = fa.coef[CF_INV1 * CSTR + gg], mu1 = fa.coef[CF_MU1 * CSTR + gg];
         const double dg1 = inv1 * (dyu - mu1 * db1);
         db1s[gg] = db1; dg1s[gg] = dg1;
-        grads[g.o_b1 + gg] = (float)db1;
-        grads[g.o_g1 + gg] = (float)dg1;
+        fa.grads[g.o_b1 + gg] = (float)db1;
+        fa.grads[g.o_g1 + gg] = (float)dg1;
     }
     __syncthreads();
-    for (int p = tid; p < g.F1 * K1; p += 256) {
+    const double n1 = (double)g.B * g.C * g.T;
+    for (int p = tid; p < F1 * K1; p += NTH) {
         const int gg = p / K1, k = p - gg * K1;
-        const float* w = prm + g.o_w1 + gg * K1;
+        const double* w = wd + gg * K1;
         double qg = 0.0;
         for (int o = gg * g.D; o < (gg + 1) * g.D; ++o) qg += Q[o * K1 + k];
         double ux = 0.0;
-        for (int l = 0; l < K1; ++l) ux += (double)w[l] * Gm[l * K1 + k];
-        const double inv1 = coef[CF_INV1 * CSTR + gg], mu1 = coef[CF_MU1 * CSTR + gg];
+        for (int l = 0; l < K1; ++l) ux += w[l] * Gm[l * K1 + k];
+        const double inv1 = fa.coef[CF_INV1 * CSTR + gg], mu1 = fa.coef[CF_MU1 * CSTR + gg];
         const double xhx = inv1 * (ux - mu1 * S1[k]);
-        const double a1 = coef[CF_A1 * CSTR + gg];
+        const double a1 = fa.coef[CF_A1 * CSTR + gg];
         const double v = a1 * (qg - db1s[gg] / n1 * S1[k] - dg1s[gg] / n1 * xhx);
-        grads[g.o_w1 + p] = (float)v;
+        fa.grads[g.o_w1 + p] = (float)v;
     }
+    if (!fa.adam_m) return;
+    __syncthreads();                  // this workgroup's gradient stores are visible to all its waves
+    const int s = *fa.step + 1;
+    const float step_size = (float)((double)fa.lr / (1.0 - pow((double)fa.b1, (double)s)));
+    const float bc2s = (float)sqrt(1.0 - pow((double)fa.b2, (double)s));
+    for (int i = tid; i < g.nparam; i += NTH)
+        adam_elem(fa.params + i, fa.grads[i], fa.adam_m + i, fa.adam_v + i, fa.b1, fa.b2, step_size,
+                  bc2s, fa.eps);
+    __syncthreads();
+    if (tid == 0) *fa.step = s;
 }
 
 // torch.optim.Adam (weight_decay=0, amsgrad=False): torch/optim/adam.py:457,476,531-547
@@ -270,16 +342,9 @@ __global__ __launch_bounds__(256) void k_adam(int64_t n, float* __restrict__ p, 
     const int s = *step + 1;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n) {
-        const float g = gr[i];
-        const float mi = m[i] + (1.f - b1) * (g - m[i]);
-        const float vi = b2 * v[i] + (1.f - b2) * g * g;
-        m[i] = mi; v[i] = vi;
-        const double bc1 = 1.0 - pow((double)b1, (double)s);
-        const double bc2 = 1.0 - pow((double)b2, (double)s);
-        const float step_size = (float)(lr / bc1);
-        const float bc2s = (float)sqrt(bc2);
-        const float denom = sqrtf(vi) / bc2s + eps;
-        p[i] = p[i] - step_size * (mi / denom);
+        const float step_size = (float)((double)lr / (1.0 - pow((double)b1, (double)s)));
+        const float bc2s = (float)sqrt(1.0 - pow((double)b2, (double)s));
+        adam_elem(p + i, gr[i], m + i, v + i, b1, b2, step_size, bc2s, eps);
     }
 }
 

@@ -20,8 +20,11 @@ static int fail(int code, const char* fmt, ...) {
 static inline int rup(int a, int m) { return (a + m - 1) / m * m; }
 static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
 
+enum { TK_A = 0, TK_B, TK_C, TK_D, TK_E, TK_COUNT };
+constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 320 B, a multiple of 16
+
 struct WsLayout {
-    size_t partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, total;
+    size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, total;
 };
 
 static int device_cus() {
@@ -89,6 +92,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nD = g->F2 * g->F2 + 18 * g->F2;
     g->nE = g->F2 * g->K1 + g->F2 * g->C + 2 * g->F2;
     g->grid = std::min(g->B, device_cus());
+    g->rgs = std::max(32, (g->grid + NGRPMAX - 1) / NGRPMAX);
+    g->ngrp = (g->grid + g->rgs - 1) / g->rgs;
     const int rows1 = g->C * g->RS;                   // x rows (A, B, infer: one buffer)
     const int rows2 = 2 * g->C * g->RS;               // double-buffered x rows (E)
     const int nf4 = rup(g->NF, 4);
@@ -100,6 +105,13 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->xdb = (g->ldsE + rows2) * 4 <= 160 * 1024 ? 1 : 0;
     g->ldsE = std::max(g->ldsE + (g->xdb ? rows2 : rows1), NWAVE * 256);
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
+    // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
+    auto tail = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + std::max(tail_scratch_doubles(ncols), fin)); };
+    g->ldsA = std::max(g->ldsA, tail(g->nA, fin1_scratch_doubles(g->K1, g->F1)));
+    g->ldsB = std::max(g->ldsB, tail(g->nB, 0));
+    g->ldsC = std::max(g->ldsC, tail(g->nC, 0));
+    g->ldsD = std::max(g->ldsD, tail(g->nD, 0));
+    g->ldsE = std::max(g->ldsE, tail(g->nE, fin5_scratch_doubles(g->K1, g->F1)));
     if (launch) {
         if (g->F2 > F2MAX)
             return fail(EEGNET_EINVAL, "F1*D = %d > %d: the row-per-wave train step covers F2 <= %d "
@@ -120,13 +132,14 @@ static WsLayout make_layout(const Geo& g) {
     WsLayout L;
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = rupz(o + bytes, 256); return r; };
+    L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
     L.partA = take((size_t)g.grid * g.nA * 4);
     L.partB = take((size_t)g.grid * g.nB * 4);
     L.partC = take((size_t)g.grid * g.nC * 4);
     L.partD = take((size_t)g.grid * g.nD * 4);
     L.partE = take((size_t)g.grid * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
-    L.sums = take((size_t)nmax * 8 * RCH);
+    L.sums = take((size_t)nmax * 8 * NGRPMAX);
     L.stats = take((size_t)(g.K1 * g.K1 + g.K1) * 8);
     L.coef = take((size_t)CF_COUNT * CSTR * 4);
     const size_t per = (size_t)g.B * g.F2 * g.T1 * 4;
@@ -144,9 +157,9 @@ static uint64_t mix_key(uint64_t seed, uint64_t offset) {
 }
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
-enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_COLSUM, KID_FIN, KID_ADAM, KID_INFER, KID_COUNT };
+enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
-                                              "k_colsum", "k_fin", "k_adam", "k_infer"};
+                                              "k_adam", "k_infer", "memset_tickets"};
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { bool on = false; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
@@ -193,7 +206,6 @@ static void ensure_attrs() {
     set_attrs_shape<64, 0, 0, 0>();
     set_attrs_shape<32, 22, 256, 16>();
     set_attrs_shape<32, 22, 257, 16>();
-    hipFuncSetAttribute((const void*)k_fin1, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
     g_attr_done = true;
 }
 
@@ -206,73 +218,75 @@ static void ensure_attrs() {
         else { LAUNCH(K1_, 0, 0, 0); }                                                           \
     } while (0)
 
-static int colsum(const float* part, int nrows, int ncols, double* out, hipStream_t s) {
-    PROF(KID_COLSUM);
-    hipLaunchKernelGGL(k_colsum, dim3((ncols + 63) / 64, RCH), dim3(256), 0, s, part, nrows, ncols, out);
-    LAUNCH_CHECK("k_colsum");
+// the finalize arguments of one pass (ticket words `tk`); Adam is attached to pass E by the caller
+static FinArgs fin_args(const WsLayout& L, char* ws, int tk, float* bn, float* grads, float* loss,
+                        int update_running, int ce) {
+    FinArgs f;
+    memset(&f, 0, sizeof(f));
+    f.part2 = (double*)(ws + L.sums);
+    f.cnt = (unsigned*)(ws + L.cnt) + tk * NCNT;
+    f.stats = (double*)(ws + L.stats);
+    f.coef = (float*)(ws + L.coef);
+    f.bn = bn; f.grads = grads; f.loss = loss;
+    f.update_running = update_running; f.ce = ce;
+    return f;
+}
+
+// zero the ticket words (cdna_hip_programming.md §6 Guideline 16: re-initialise every call)
+static int reset_tickets(const WsLayout& L, char* ws, hipStream_t s) {
+    PROF(KID_MEMSET);
+    if (hipMemsetAsync(ws + L.cnt, 0, CNT_BYTES, s) != hipSuccess)
+        return fail(EEGNET_ELAUNCH, "hipMemsetAsync(tickets): %s", hipGetErrorString(hipGetLastError()));
     return 0;
 }
 
 template <int K1>
 static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
-                       const float* x, const uint8_t* m2, float* logits, int update_running,
-                       int c_mode, const int64_t* labels, float* loss, float* grads, hipStream_t s) {
-    double* sums = (double*)(ws + L.sums);
-    float* coef = (float*)(ws + L.coef);
+                       const float* x, const uint8_t* m2, int update_running, hipStream_t s) {
+    const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
+    const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0);
 #define LAUNCH_A(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsA * 4, s, \
-                                                   g, params, x, (float*)(ws + L.partA))
+                                                   g, params, x, (float*)(ws + L.partA), fa)
     { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
     } LAUNCH_CHECK("k_pass_a");
-    if (int r = colsum((float*)(ws + L.partA), g.grid, g.nA, sums, s)) return r;
-    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin1, dim3(1), dim3(256), (g.K1 * g.K1 + g.K1 + 128 + g.nA) * 8, s, g, params, sums,
-                       (double*)(ws + L.stats), coef, bn, update_running);
-    } LAUNCH_CHECK("k_fin1");
 #define LAUNCH_B(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsB * 4, s, \
-                       g, params, coef, x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), (float*)(ws + L.E2), \
-                       (float*)(ws + L.partB))
+                       g, params, (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), \
+                       (float*)(ws + L.E2), (float*)(ws + L.partB), fb)
     { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
     } LAUNCH_CHECK("k_pass_b");
-    if (int r = colsum((float*)(ws + L.partB), g.grid, g.nB, sums, s)) return r;
-    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin2, dim3(1), dim3(256), g.nB * 8, s, g, sums, coef, bn, update_running);
-    } LAUNCH_CHECK("k_fin2");
-    (void)labels; (void)loss; (void)grads; (void)c_mode; (void)logits;
     return 0;
 }
 
+// adam: nullptr = gradients only
 template <int K1>
-static int run_backward(const Geo& g, const WsLayout& L, char* ws, const float* params,
+static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params,
                         const float* x, const uint8_t* m2, const uint8_t* m3, const float* dlogits,
                         const int64_t* labels, float* logits, float* grads, float* loss, int c_mode,
-                        hipStream_t s) {
-    double* sums = (double*)(ws + L.sums);
-    float* coef = (float*)(ws + L.coef);
-    float* dl = dlogits ? (float*)dlogits : (float*)(ws + L.dl);
+                        const FinArgs* adam, hipStream_t s) {
+    const float* coef = (const float*)(ws + L.coef);
+    const float* dl = dlogits ? dlogits : (const float*)(ws + L.dl);
+    const FinArgs fc = fin_args(L, ws, TK_C, nullptr, grads, loss, 0, (c_mode & PC_CE) ? 1 : 0);
+    const FinArgs fd = fin_args(L, ws, TK_D, nullptr, grads, nullptr, 0, 0);
+    FinArgs fe = fin_args(L, ws, TK_E, nullptr, grads, nullptr, 0, 0);
+    if (adam) {
+        fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
+        fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
+    }
 #define LAUNCH_CB(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsC * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
-                       (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode)
+                       (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fc)
     { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
     } LAUNCH_CHECK("k_pass_c(bwd)");
-    if (int r = colsum((float*)(ws + L.partC), g.grid, g.nC, sums, s)) return r;
-    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin3, dim3(1), dim3(256), g.nC * 8, s, g, params, sums, coef, grads, loss,
-                       (c_mode & PC_CE) ? 1 : 0);
-    } LAUNCH_CHECK("k_fin3");
 #define LAUNCH_D(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
-                       (const float*)(ws + L.E2), m2, m3, (const float*)dl, (float*)(ws + L.dp2), \
-                       (float*)(ws + L.partD))
+                       (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2), \
+                       (float*)(ws + L.partD), fd)
     { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
     } LAUNCH_CHECK("k_pass_d");
-    if (int r = colsum((float*)(ws + L.partD), g.grid, g.nD, sums, s)) return r;
-    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin4, dim3(1), dim3(256), g.nD * 8, s, g, params, sums, coef, grads);
-    } LAUNCH_CHECK("k_fin4");
 #define LAUNCH_E(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsE * 4, s, \
-                       g, params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE))
+                       g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe)
     { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
     } LAUNCH_CHECK("k_pass_e");
-    if (int r = colsum((float*)(ws + L.partE), g.grid, g.nE, sums, s)) return r;
-    { PROF(KID_FIN); hipLaunchKernelGGL(k_fin5, dim3(1), dim3(256), g.nE * 8, s, g, params, sums, (const double*)(ws + L.stats),
-                       (const float*)coef, grads);
-    } LAUNCH_CHECK("k_fin5");
     return 0;
 }
 
@@ -314,12 +328,15 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
-    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, mask2, logits, 1, 0, nullptr, nullptr, nullptr, s)
-                       : run_forward<64>(g, L, w, params, bn_buffers, x, mask2, logits, 1, 0, nullptr, nullptr, nullptr, s);
+    if (int r = reset_tickets(L, w, s)) return r;
+    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, mask2, 1, s)
+                       : run_forward<64>(g, L, w, params, bn_buffers, x, mask2, 1, s);
     if (r) return r;
+    FinArgs none;
+    memset(&none, 0, sizeof(none));
 #define LAUNCH_CF(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsC * 4, s, \
                        g, params, (const float*)(w + L.coef), (const float*)(w + L.d2), mask3, (const float*)nullptr, \
-                       (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS)
+                       (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS, none)
     { PROF(KID_C);
       if (g.K1 == 32) EEG_DISPATCH(32, g, LAUNCH_CF); else EEG_DISPATCH(64, g, LAUNCH_CF);
     } LAUNCH_CHECK("k_pass_c(fwd)");
@@ -342,9 +359,11 @@ int eegnet_backward(const eegnet_dims* dims, const float* params, const float* x
     const WsLayout L = make_layout(g);
     const int mode = PC_BWD | (dlogits ? 0 : PC_CE);
     hipStream_t s = (hipStream_t)stream;
+    if (int r = reset_tickets(L, (char*)ws, s)) return r;
+    float* p = const_cast<float*>(params);        // written only by a fused Adam, which this call has not
     return g.K1 == 32
-        ? run_backward<32>(g, L, (char*)ws, params, x, mask2, mask3, dlogits, labels, nullptr, grads, loss, mode, s)
-        : run_backward<64>(g, L, (char*)ws, params, x, mask2, mask3, dlogits, labels, nullptr, grads, loss, mode, s);
+        ? run_backward<32>(g, L, (char*)ws, p, x, mask2, mask3, dlogits, labels, nullptr, grads, loss, mode, nullptr, s)
+        : run_backward<64>(g, L, (char*)ws, p, x, mask2, mask3, dlogits, labels, nullptr, grads, loss, mode, nullptr, s);
 }
 
 int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const float* bn_buffers,
@@ -394,17 +413,21 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
-    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, nullptr, 1, 0, nullptr, nullptr, nullptr, s)
-                       : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, nullptr, 1, 0, nullptr, nullptr, nullptr, s);
+    if (int r = reset_tickets(L, w, s)) return r;
+    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, 1, s)
+                       : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, 1, s);
     if (r) return r;
     const int mode = PC_BWD | PC_CE | (logits ? PC_LOGITS : 0);
-    r = g.K1 == 32
-        ? run_backward<32>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, s)
-        : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, s);
-    if (r) return r;
-    if (!adam_state) return 0;       // gradients only (data-parallel: all-reduce, clamp, then Adam)
-    return eegnet_adam_step(g.nparam, params, grads, adam_state, adam_state + g.nparam, step, lr,
-                            beta1, beta2, eps, stream);
+    // Adam runs in pass E's finalize; adam_state == NULL: gradients only (data-parallel: all-reduce,
+    // clamp, then eegnet_adam_step)
+    FinArgs adam;
+    memset(&adam, 0, sizeof(adam));
+    adam.adam_m = adam_state; adam.adam_v = adam_state ? adam_state + g.nparam : nullptr; adam.step = step;
+    adam.lr = lr; adam.b1 = beta1; adam.b2 = beta2; adam.eps = eps;
+    const FinArgs* ap = adam_state ? &adam : nullptr;
+    return g.K1 == 32
+        ? run_backward<32>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, ap, s)
+        : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, ap, s);
 }
 
 int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream) {
@@ -452,7 +475,8 @@ int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, 
 
 const char* eegnet_build_info(void) {
     return "libeegnet_hip: gfx950 (CDNA4), fp32 VALU FIR/Gram + f32 MFMA 16x16x4 GEMMs, "
-           "5-pass restructured EEGNet train step, 1024-thread row-per-wave workgroups";
+           "5-pass restructured EEGNet train step, 1024-thread row-per-wave workgroups, "
+           "in-kernel ticketed fp64 reductions + finalize";
 }
 
 }  // extern "C"

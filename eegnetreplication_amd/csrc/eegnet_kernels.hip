@@ -13,8 +13,8 @@
 //     y2[o,t] = a1[g] v[o,t] + c1[g] sum_c ws[o,c]         (BN1 affine folded: a1 = g1/sd1)
 // BN1's batch statistics come from the lag-Gram of x and window sums; BN2's from sum v, sum v^2.
 // Every backward weight-gradient reduction is linear in dy2 and is written as per-trial partial sums
-// that finalize kernels combine with the BN constants at the end.  Five streaming passes (A..E), each
-// followed by a deterministic fp64 column reduction and a one-workgroup finalize:
+// that finalize code combines with the BN constants at the end.  Five streaming passes (A..E); each
+// ends in a ticketed deterministic fp64 reduction whose last workgroup runs the pass's finalize:
 //   A  x -> lag-Gram / edge / window sums of x, sum v, sum v^2              (BN1, BN2 statistics)
 //   B  x -> v -> BN2 -> ELU -> pool4 -> dropout -> d2, dw16, pw -> sum r, r^2 (BN3 statistics)
 //   C  d2 -> block2 -> BN3 -> ELU -> pool8 -> dropout -> FC -> logits [-> CE, dFC, BN3-bwd sums]
@@ -34,6 +34,6 @@
 
 #include "../../include/eegnet_abi.h"
 #include "eegnet_common.h"
-#include "eegnet_passes.hip"
 #include "eegnet_finalize.hip"
+#include "eegnet_passes.hip"
 #include "eegnet_host.hip"

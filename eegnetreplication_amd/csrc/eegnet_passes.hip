@@ -20,7 +20,8 @@ namespace eeg {
 // ================================================================================================
 template <int K1, int CC, int TT, int FF>
 __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__ prm,
-                                                const float* __restrict__ x, float* __restrict__ part) {
+                                                const float* __restrict__ x, float* __restrict__ part,
+                                                FinArgs fa) {
     using G_ = KG<K1>;
     EEG_DIMS(g);
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -156,18 +157,20 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
     if (tid <= K1) {
         float t = 0.f;
         for (int w = 0; w < NWAVE; ++w) t += red[w * (K1 + 1) + tid];
-        row[tid] = t;
+        pub(row + (tid), t);
     }
 #pragma unroll
     for (int i = 0; i < G_::NEI; ++i)
-        if (ea[i] != -2 && tid + NTH * i < g.nedge) row[K1 + 1 + tid + NTH * i] = eacc[i];
+        if (ea[i] != -2 && tid + NTH * i < g.nedge) pub(row + (K1 + 1 + tid + NTH * i), eacc[i]);
     {
         const float a = wave_sum(sv), a2 = wave_sum(sv2);
         if (fir_on && lane == 0) {
-            row[K1 + 1 + g.nedge + o] = a;
-            row[K1 + 1 + g.nedge + F2 + o] = a2;
+            pub(row + (K1 + 1 + g.nedge + o), a);
+            pub(row + (K1 + 1 + g.nedge + F2 + o), a2);
         }
     }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nA, fa, dsm)) fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa);
 }
 
 // ================================================================================================
@@ -176,11 +179,12 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
 // ================================================================================================
 template <int K1, int CC, int TT, int FF>
 __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__ prm,
-                                                const float* __restrict__ coef,
+                                                const float* coef,    // the finalize writes it: no __restrict__
                                                 const float* __restrict__ x,
                                                 const uint8_t* __restrict__ mask2,
                                                 float* __restrict__ d2g, float* __restrict__ E1g,
-                                                float* __restrict__ E2g, float* __restrict__ part) {
+                                                float* __restrict__ E2g, float* __restrict__ part,
+                                                FinArgs fa) {
     using G_ = KG<K1>;
     EEG_DIMS(g);
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -274,9 +278,11 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
     const float a = wave_sum(sr), a2 = wave_sum(sr2);
     if (row_on && lane == 0) {
         float* row = part + (size_t)blockIdx.x * g.nB;
-        row[o] = a;
-        row[F2 + o] = a2;
+        pub(row + (o), a);
+        pub(row + (F2 + o), a2);
     }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nB, fa, dsm)) fin2(g, dsm + 2, fa);
 }
 
 // block_2 forward of one trial in the row-per-wave layout: D2s (padded d2 rows) -> q (Qs) -> r.
@@ -319,13 +325,13 @@ __device__ __forceinline__ void block2_rows(int F2, int T1, int RS2, const float
 // ================================================================================================
 template <int K1, int CC, int TT, int FF>
 __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__ prm,
-                                                const float* __restrict__ coef,
+                                                const float* coef,    // the finalize writes it: no __restrict__
                                                 const float* __restrict__ d2g,
                                                 const uint8_t* __restrict__ mask3,
                                                 const float* __restrict__ dlin,
                                                 const int64_t* __restrict__ labels,
                                                 float* __restrict__ logits, float* __restrict__ dlout,
-                                                float* __restrict__ part, int mode) {
+                                                float* __restrict__ part, int mode, FinArgs fa) {
     EEG_DIMS(g);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2s = sm;
@@ -460,15 +466,17 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
 #pragma unroll
         for (int i = 0; i < MAXW; ++i) {
             const int p = tid + NTH * i;
-            if (p < NCLS * NF) row[p] = wacc[i];
+            if (p < NCLS * NF) pub(row + (p), wacc[i]);
         }
-        if (tid < NCLS) row[NCLS * NF + tid] = bacc;
+        if (tid < NCLS) pub(row + (NCLS * NF + tid), bacc);
         const float a = wave_sum(sdz), ax = wave_sum(sdzx);
         if (row_on && lane == 0) {
-            row[NCLS * NF + NCLS + o] = a;
-            row[NCLS * NF + NCLS + F2 + o] = ax;
+            pub(row + (NCLS * NF + NCLS + o), a);
+            pub(row + (NCLS * NF + NCLS + F2 + o), ax);
         }
-        if (tid == 0) row[NCLS * NF + NCLS + 2 * F2] = lossacc;
+        if (tid == 0) pub(row + (NCLS * NF + NCLS + 2 * F2), lossacc);
+        double* dsm = (double*)sm;
+        if (grid_reduce(g, part, g.nC, fa, dsm)) fin3(g, prm, dsm + 2, fa);
     }
 }
 
@@ -478,14 +486,15 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
 // ================================================================================================
 template <int K1, int CC, int TT, int FF>
 __global__ __launch_bounds__(NTH) void k_pass_d(Geo g, const float* __restrict__ prm,
-                                                const float* __restrict__ coef,
+                                                const float* coef,    // the finalize writes it: no __restrict__
                                                 const float* __restrict__ d2g,
                                                 const float* __restrict__ E1g,
                                                 const float* __restrict__ E2g,
                                                 const uint8_t* __restrict__ mask2,
                                                 const uint8_t* __restrict__ mask3,
                                                 const float* __restrict__ dl,
-                                                float* __restrict__ dp2g, float* __restrict__ part) {
+                                                float* __restrict__ dp2g, float* __restrict__ part,
+                                                FinArgs fa) {
     EEG_DIMS(g);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2s = sm;
@@ -612,18 +621,20 @@ __global__ __launch_bounds__(NTH) void k_pass_d(Geo g, const float* __restrict__
 #pragma unroll
     for (int i = 0; i < F2MAX; ++i) {
         const float a = wave_sum(dW3p[i]);
-        if (row_on && lane == 0 && i < F2) row[o * F2 + i] = a;
+        if (row_on && lane == 0 && i < F2) pub(row + (o * F2 + i), a);
     }
 #pragma unroll
     for (int k = 0; k < K2; ++k) {
         const float a = wave_sum(dw2p[k]);
-        if (row_on && lane == 0) row[F2 * F2 + o * K2 + k] = a;
+        if (row_on && lane == 0) pub(row + (F2 * F2 + o * K2 + k), a);
     }
     const float a = wave_sum(sz), ax = wave_sum(szx);
     if (row_on && lane == 0) {
-        row[F2 * F2 + 16 * F2 + o] = a;
-        row[F2 * F2 + 17 * F2 + o] = ax;
+        pub(row + (F2 * F2 + 16 * F2 + o), a);
+        pub(row + (F2 * F2 + 17 * F2 + o), ax);
     }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nD, fa, dsm)) fin4(g, prm, dsm + 2, fa);
 }
 
 // ================================================================================================
@@ -631,11 +642,11 @@ __global__ __launch_bounds__(NTH) void k_pass_d(Geo g, const float* __restrict__
 // part row: [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2]
 // ================================================================================================
 template <int K1, int CC, int TT, int FF>
-__global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* __restrict__ prm,
-                                                const float* __restrict__ coef,
+__global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Adam (finalize) writes it
+                                                const float* coef,    // the finalize writes it: no __restrict__
                                                 const float* __restrict__ x,
                                                 const float* __restrict__ dp2g,
-                                                float* __restrict__ part) {
+                                                float* __restrict__ part, FinArgs fa) {
     using G_ = KG<K1>;
     EEG_DIMS(g);
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -774,13 +785,13 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* __restrict__
 #pragma unroll
     for (int k = 0; k < K1; ++k) {
         const float a = wave_sum(Q[k]);
-        if (row_on && lane == 0) row[o * K1 + k] = a;
+        if (row_on && lane == 0) pub(row + (o * K1 + k), a);
     }
     {
         const float a = wave_sum(sdy), a2 = wave_sum(sdyv);
         if (row_on && lane == 0) {
-            row[F2 * K1 + F2 * C + o] = a;
-            row[F2 * K1 + F2 * C + F2 + o] = a2;
+            pub(row + (F2 * K1 + F2 * C + o), a);
+            pub(row + (F2 * K1 + F2 * C + F2 + o), a2);
         }
     }
     // Xm: wave -> 16x16 tile partial (rows 4lk+r, col li) -> LDS [wave][256] -> sum over the
@@ -793,8 +804,10 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* __restrict__
         const int ct2 = c >> 4, cc = c & 15;
         float a = 0.f;
         for (int w = ct2 * wpc; w < (ct2 + 1) * wpc; ++w) a += red[w * 256 + oo2 * 16 + cc];
-        row[F2 * K1 + p] = a;
+        pub(row + (F2 * K1 + p), a);
     }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nE, fa, dsm)) fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa);
 }
 
 // ================================================================================================
