@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libeegnet_hip.so")
+# EEGNET_LIB selects a variant built beside it (e.g. libeegnet_hip_trace.so for tools/trace_step.py)
+LIB_PATH = os.path.join(_HERE, os.environ.get("EEGNET_LIB", "libeegnet_hip.so"))
 
 _lock = threading.Lock()
 _lib = None
@@ -45,6 +46,8 @@ _SIGS = {
                                          _vp, _vp, ctypes.c_int]),
     "eegnet_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "eegnet_profile_collect": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp, ctypes.c_int, _vp]),
+    "eegnet_trace_enable": (ctypes.c_int, [_vp]),
+    "eegnet_trace_bytes": (ctypes.c_size_t, []),
     "eegnet_last_error": (ctypes.c_char_p, []),
     "eegnet_build_info": (ctypes.c_char_p, []),
 }

@@ -18,6 +18,7 @@ constexpr int NCLS = 4;       // classes (model.py:80)
 constexpr int LP2 = 8;        // left pad of d2 / dq rows in LDS (>= 7, multiple of 4)
 constexpr int MAXPF = 16;     // prefetch registers per thread: C*T <= NTH*MAXPF floats
 constexpr int F2MAX = 16;     // rows per trial plane this build keeps one-per-wave
+constexpr int MAXT1Q = 4;     // pooled samples per lane: T1 = T/4 <= 256 (T <= 1024)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -54,7 +55,40 @@ struct Geo {
     int rgs, ngrp;       // in-kernel reduction: partial rows per group, groups (<= NGRPMAX)
     // LDS (floats)
     int ldsA, ldsB, ldsC, ldsD, ldsE, ldsI;
+    // optional timeline instrumentation (eegnet_trace_enable): [pass][workgroup][TR_SLOTS] stamps
+    unsigned long long* trace;
 };
+
+// timeline stamps: wall clock (100 MHz) at kernel phase boundaries, shader-clock phase sums (loop)
+constexpr int TR_SLOTS = 16, TR_MAXWG = 2048;
+enum TraceEv { TR_ENTRY = 0, TR_PRO, TR_LOOP, TR_PUB, TR_GRP, TR_TOP, TR_FIN, TR_PH0 = 8 };
+// compiled in only with -DEEGNET_TRACE (libeegnet_hip_trace.so, tools/trace_step.py)
+#ifdef EEGNET_TRACE
+#define TRACE_ON(g_) ((g_).trace != nullptr)
+#else
+#define TRACE_ON(g_) false
+#endif
+#define TRACE(g_, pass_, ev_)                                                                    \
+    do {                                                                                         \
+        if (TRACE_ON(g_) && threadIdx.x == 0)                                                      \
+            (g_).trace[((size_t)(pass_) * TR_MAXWG + blockIdx.x) * TR_SLOTS + (ev_)] = wall_clock64(); \
+    } while (0)
+#define TRACE_PH(g_, pass_, ph_, t0_)                                                            \
+    do {                                                                                         \
+        if (TRACE_ON(g_) && threadIdx.x == 0) {                                                  \
+            const unsigned long long t1_ = clock64();                                            \
+            tacc_[ph_] += t1_ - (t0_);                                                           \
+            (t0_) = t1_;                                                                         \
+        }                                                                                        \
+    } while (0)
+// loop-end stamp plus the register-held phase sums
+#define TRACE_LOOP(g_, pass_)                                                                    \
+    do {                                                                                         \
+        TRACE(g_, pass_, TR_LOOP);                                                               \
+        if (TRACE_ON(g_) && threadIdx.x == 0)                                                    \
+            for (int ph_ = 0; ph_ < 8; ++ph_)                                                    \
+                (g_).trace[((size_t)(pass_) * TR_MAXWG + blockIdx.x) * TR_SLOTS + TR_PH0 + ph_] = tacc_[ph_]; \
+    } while (0)
 
 // coefficient block layout (float, CSTR per field; F1, F2 <= 64)
 enum CoefField {
@@ -79,6 +113,7 @@ struct FinArgs {
     float* grads;
     float* loss;
     int update_running, ce;
+    int tpass;                    // pass index for the timeline stamps
     // Adam (torch.optim.Adam) fused into pass E's finalize when adam_m != nullptr
     float* params;
     float* adam_m;
@@ -133,10 +168,57 @@ __device__ __forceinline__ float keep_mul(const Geo& g, const uint8_t* __restric
     return u >= g.p ? g.scale : 0.f;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---- cross-lane reductions: v_permlane32/16_swap halving + DPP within 16-lane rows ----
+// (the builtins' second result is mis-compiled by this toolchain -- it returns the first result
+// twice -- so the swaps are inline asm; tools/lane_ops_check.hip pins the operand semantics:
+// swap32 a.hi <-> b.lo, swap16 a.rows{1,3} <-> b.rows{0,2})
+__device__ __forceinline__ void swap32(float& a, float& b) {
+    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void swap16(float& a, float& b) {
+    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// every lane gets the sum over its 16-lane row: quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, 8
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x124>(v);
+    v += dpp<0x128>(v);
     return v;
+}
+
+// sum over the 64 lanes, result in every lane
+__device__ __forceinline__ float wave_sum(float v) {
+    float a = v, b = v;
+    swap32(a, b);
+    v = a + b;
+    a = v; b = v;
+    swap16(a, b);
+    return row_sum16(a + b);
+}
+
+// N independent 64-lane sums at once (N % 4 == 0): two halving swaps then 4 DPP steps on N/4
+// registers (~2.5 instructions per value instead of 6 dependent shuffles).  On return, lane
+// 16*r (r < 4) holds sum[j + r*N/4] in v[j] for j < N/4 (every lane of row r holds the same).
+template <int N>
+__device__ __forceinline__ void wave_reduce(float (&v)[N]) {
+    static_assert(N % 4 == 0, "wave_reduce: N must be a multiple of 4");
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+        swap32(v[i], v[i + N / 2]);
+        v[i] += v[i + N / 2];
+    }
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) {
+        swap16(v[j], v[j + N / 4]);
+        v[j] += v[j + N / 4];
+    }
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) v[j] = row_sum16(v[j]);
 }
 
 // order this wave's LDS writes before its later LDS reads (rows a wave owns need no block barrier)

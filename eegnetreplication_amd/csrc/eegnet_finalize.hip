@@ -55,6 +55,8 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     double* scr = dsm + tail_s_doubles(ncols);
     const int grp = blockIdx.x / g.rgs;
     const int r0 = grp * g.rgs, r1 = min(g.grid, r0 + g.rgs), nr = r1 - r0;
+    const int tp = fa.tpass;
+    TRACE(g, tp, TR_PUB);
     if (!take_ticket(fa.cnt + grp, (unsigned)nr, flag)) return false;
     // group reducer: rows [r0, r1), rs interleaved row subsets per column, then the rs-way sum
     const int rs = max(1, min(nr, NTH / ncols));
@@ -79,6 +81,7 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
         for (int sub = 0; sub < rs; ++sub) a += scr[sub * ncols + c];
         pub(fa.part2 + (size_t)grp * ncols + c, a);
     }
+    TRACE(g, tp, TR_GRP);
     if (!take_ticket(fa.cnt + (NCNT - 1), (unsigned)g.ngrp, flag)) return false;
     for (int c = tid; c < ncols; c += NTH) {
         double v[NGRPMAX];
@@ -93,6 +96,7 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     if (tid < g.ngrp) __hip_atomic_store(fa.cnt + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) __hip_atomic_store(fa.cnt + (NCNT - 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
+    TRACE(g, tp, TR_TOP);
     return true;
 }
 

@@ -38,9 +38,22 @@ static int device_cus() {
     return cus;
 }
 
+// workgroups resident per CU for the streaming passes (EEGNET_WGPC, default 1; experiment knob)
+static int wg_per_cu() {
+    static int v = 0;
+    if (v == 0) {
+        const char* e = getenv("EEGNET_WGPC");
+        v = e ? std::max(1, std::min(2, atoi(e))) : 1;
+    }
+    return v;
+}
+
+static unsigned long long* g_trace_buf = nullptr;     // eegnet_trace_enable
+
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     if (!d) return fail(EEGNET_EINVAL, "dims is NULL");
     memset(g, 0, sizeof(*g));
+    g->trace = g_trace_buf;
     g->B = d->B; g->C = d->C; g->T = d->T; g->F1 = d->F1; g->D = d->D; g->K1 = d->K1;
     g->F2 = d->F1 * d->D;
     if (g->B < 1) return fail(EEGNET_EINVAL, "B must be >= 1 (got %d)", g->B);
@@ -91,7 +104,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nC = NCLS * g->NF + NCLS + 2 * g->F2 + 1;
     g->nD = g->F2 * g->F2 + 18 * g->F2;
     g->nE = g->F2 * g->K1 + g->F2 * g->C + 2 * g->F2;
-    g->grid = std::min(g->B, device_cus());
+    g->grid = std::min(g->B, device_cus() * wg_per_cu());
     g->rgs = std::max(32, (g->grid + NGRPMAX - 1) / NGRPMAX);
     g->ngrp = (g->grid + g->rgs - 1) / g->rgs;
     const int rows1 = g->C * g->RS;                   // x rows (A, B, infer: one buffer)
@@ -102,7 +115,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->ldsC = 2 * g->F2 * g->RS2 + 2 * nf4 + 8;
     g->ldsD = 4 * g->F2 * g->RS2 + nf4;
     g->ldsE = 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4);
-    g->xdb = (g->ldsE + rows2) * 4 <= 160 * 1024 ? 1 : 0;
+    g->xdb = (wg_per_cu() == 1 && (g->ldsE + rows2) * 4 <= 160 * 1024) ? 1 : 0;
     g->ldsE = std::max(g->ldsE + (g->xdb ? rows2 : rows1), NWAVE * 256);
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
@@ -120,6 +133,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
             return fail(EEGNET_EINVAL, "C*T = %d exceeds the %d-float prefetch of one trial", g->C * g->T,
                         NTH * MAXPF);
         if (g->T1 > 64 * MAXT1Q) return fail(EEGNET_EINVAL, "T/4 > %d", 64 * MAXT1Q);
+        if (g->F2 * g->T1 > 4 * NTH) return fail(EEGNET_EINVAL, "F2*(T/4) > %d", 4 * NTH);
         if (NCLS * g->NF > 4 * NTH) return fail(EEGNET_EINVAL, "F2*(T/32) too large");
         const int lmax = std::max(std::max(std::max(g->ldsA, g->ldsB), std::max(g->ldsC, g->ldsD)),
                                   std::max(g->ldsE, g->ldsI));
@@ -229,6 +243,7 @@ static FinArgs fin_args(const WsLayout& L, char* ws, int tk, float* bn, float* g
     f.coef = (float*)(ws + L.coef);
     f.bn = bn; f.grads = grads; f.loss = loss;
     f.update_running = update_running; f.ce = ce;
+    f.tpass = tk;
     return f;
 }
 
@@ -442,6 +457,13 @@ int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream) {
 }
 
 const char* eegnet_last_error(void) { return g_err.c_str(); }
+
+int eegnet_trace_enable(void* buf) {
+    g_trace_buf = (unsigned long long*)buf;
+    return 0;
+}
+
+size_t eegnet_trace_bytes(void) { return (size_t)8 * TR_MAXWG * TR_SLOTS * sizeof(unsigned long long); }
 
 int eegnet_profile_enable(int on) {
     g_prof.on = on != 0;

@@ -24,6 +24,7 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
                                                 FinArgs fa) {
     using G_ = KG<K1>;
     EEG_DIMS(g);
+    TRACE(g, 0, TR_ENTRY);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* const Xb0 = sm;             // one x buffer: the next trial lands after its last reader
     float* Ss = sm + C * RS;
@@ -80,6 +81,8 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
     __syncthreads();
 
     int it = 0;
+    TRACE(g, 0, TR_PRO);
+    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = Xb0;
         float* Xn = Xb0;
@@ -125,7 +128,9 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
                 eacc[i] += acc0 + acc1;
             }
         }
+        TRACE_PH(g, 0, 0, tph_);
         __syncthreads();                                   // Ss complete
+        TRACE_PH(g, 0, 1, tph_);
         if (fir_on) {
             const float* row = Ss + o * RS;
             for (int q = lane; q < TQ; q += 64) {
@@ -138,20 +143,33 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
                     if (4 * q + i < T) { sv += v[i]; sv2 = fmaf(v[i], v[i], sv2); }
             }
         }
+        TRACE_PH(g, 0, 2, tph_);
         if (bn < g.B) x_store<PF>(pf, C, T, RS, LP, Xn, tid);
+        TRACE_PH(g, 0, 3, tph_);
         __syncthreads();                                   // Xn staged, Ss free
+        TRACE_PH(g, 0, 4, tph_);
     }
+    TRACE_LOOP(g, 0);
 
     // ---- workgroup reduction -> one partial row ----
     float* row = part + (size_t)blockIdx.x * g.nA;
-#pragma unroll
-    for (int d = 0; d < K1; ++d) {
-        const float t = wave_sum(G0[d]);
-        if (lane == 0) red[wave * (K1 + 1) + d] = t;
-    }
     {
-        const float t = wave_sum(s0);
-        if (lane == 0) red[wave * (K1 + 1) + K1] = t;
+        constexpr int NR = K1 + 4, NQ = NR / 4;       // [G0 K1][s0][sv][sv2][pad]
+        float rv[NR];
+#pragma unroll
+        for (int d = 0; d < K1; ++d) rv[d] = G0[d];
+        rv[K1] = s0; rv[K1 + 1] = sv; rv[K1 + 2] = sv2; rv[K1 + 3] = 0.f;
+        wave_reduce<NR>(rv);
+        if ((lane & 15) == 0) {
+            const int r0 = (lane >> 4) * NQ;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                const int idx = j + r0;
+                if (idx <= K1) red[wave * (K1 + 1) + idx] = rv[j];
+                else if (fir_on && idx == K1 + 1) pub(row + (K1 + 1 + g.nedge + o), rv[j]);
+                else if (fir_on && idx == K1 + 2) pub(row + (K1 + 1 + g.nedge + F2 + o), rv[j]);
+            }
+        }
     }
     __syncthreads();
     if (tid <= K1) {
@@ -162,15 +180,8 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
 #pragma unroll
     for (int i = 0; i < G_::NEI; ++i)
         if (ea[i] != -2 && tid + NTH * i < g.nedge) pub(row + (K1 + 1 + tid + NTH * i), eacc[i]);
-    {
-        const float a = wave_sum(sv), a2 = wave_sum(sv2);
-        if (fir_on && lane == 0) {
-            pub(row + (K1 + 1 + g.nedge + o), a);
-            pub(row + (K1 + 1 + g.nedge + F2 + o), a2);
-        }
-    }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nA, fa, dsm)) fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa);
+    if (grid_reduce(g, part, g.nA, fa, dsm)) { fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa); TRACE(g, 0, TR_FIN); }
 }
 
 // ================================================================================================
@@ -187,6 +198,7 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
                                                 FinArgs fa) {
     using G_ = KG<K1>;
     EEG_DIMS(g);
+    TRACE(g, 1, TR_ENTRY);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* const Xb0 = sm;             // one x buffer: the next trial lands after its last reader
     float* Ss = sm + C * RS;
@@ -222,6 +234,8 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
     __syncthreads();
 
     int it = 0;
+    TRACE(g, 1, TR_PRO);
+    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = Xb0;
         float* Xn = Xb0;
@@ -229,10 +243,16 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
         if (bn < g.B) x_prefetch<PF>(x + (size_t)bn * C * T, C, T, pf, tid);
         spatial_mfma<KS>(Xc, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
         __syncthreads();                                   // Ss complete; Qs free
+        // d2 / E1 / E2 of this row stay in registers until the next trial's x is staged: a global
+        // store issued before that x_store would hold its vmcnt wait (loads and stores drain in order)
+        float d2v[MAXT1Q], e1v[MAXT1Q], e2v[MAXT1Q];
         if (row_on) {
             const float* row = Ss + o * RS;
             float* drow = D2s + o * RS2 + LP2;
-            for (int q = lane; q < T1; q += 64) {        // pool-4 windows = quads
+#pragma unroll
+            for (int m = 0; m < MAXT1Q; ++m) {             // pool-4 windows = quads
+                const int q = lane + 64 * m;
+                if (q >= T1) break;
                 float w[4 * G_::NW];
                 lds_window<G_::NW>(row + 4 * q, w);
                 float v[4];
@@ -249,7 +269,7 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
                 }
                 const size_t gi = ((size_t)b * F2 + o) * T1 + q;
                 const float d2 = pe * 0.25f * keep_mul(g, mask2, 0, gi);
-                d2g[gi] = d2; E1g[gi] = e1; E2g[gi] = e2;
+                d2v[m] = d2; e1v[m] = e1; e2v[m] = e2;
                 drow[q] = d2;
             }
             wave_lds_fence();
@@ -263,6 +283,15 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
             }
         }
         if (bn < g.B) x_store<PF>(pf, C, T, RS, LP, Xn, tid);
+        if (row_on) {
+#pragma unroll
+            for (int m = 0; m < MAXT1Q; ++m) {
+                const int q = lane + 64 * m;
+                if (q >= T1) break;
+                const size_t gi = ((size_t)b * F2 + o) * T1 + q;
+                d2g[gi] = d2v[m]; E1g[gi] = e1v[m]; E2g[gi] = e2v[m];
+            }
+        }
         __syncthreads();                                   // Qs complete, Xn staged
         if (row_on) {                                      // pointwise F2 x F2 (model.py:62-69)
             for (int t = lane; t < T1; t += 64) {
@@ -275,19 +304,21 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
             }
         }
     }
-    const float a = wave_sum(sr), a2 = wave_sum(sr2);
-    if (row_on && lane == 0) {
-        float* row = part + (size_t)blockIdx.x * g.nB;
-        pub(row + (o), a);
-        pub(row + (F2 + o), a2);
+    TRACE_LOOP(g, 1);
+    {
+        float rv[4] = {sr, sr2, 0.f, 0.f};
+        wave_reduce<4>(rv);                        // lane 0: sum sr, lane 16: sum sr2
+        if (row_on && (lane == 0 || lane == 16)) {
+            float* row = part + (size_t)blockIdx.x * g.nB;
+            pub(row + (lane ? F2 + o : o), rv[0]);
+        }
     }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nB, fa, dsm)) fin2(g, dsm + 2, fa);
+    if (grid_reduce(g, part, g.nB, fa, dsm)) { fin2(g, dsm + 2, fa); TRACE(g, 1, TR_FIN); }
 }
 
 // block_2 forward of one trial in the row-per-wave layout: D2s (padded d2 rows) -> q (Qs) -> r.
 // Returns r[m] for t = lane + 64 m (m < MAXT1Q) of row o.  Contains one workgroup barrier.
-constexpr int MAXT1Q = 4;    // T1 <= 256 (T <= 1024)
 
 __device__ __forceinline__ void block2_rows(int F2, int T1, int RS2, const float* D2s, float* Qs,
                                             const float (&w2)[K2], const float (&w3)[F2MAX], bool row_on,
@@ -333,6 +364,7 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
                                                 float* __restrict__ logits, float* __restrict__ dlout,
                                                 float* __restrict__ part, int mode, FinArgs fa) {
     EEG_DIMS(g);
+    TRACE(g, 2, TR_ENTRY);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2s = sm;
     float* Qs = D2s + F2 * RS2;
@@ -368,6 +400,8 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
     }
     __syncthreads();
 
+    TRACE(g, 2, TR_PRO);
+    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -383,9 +417,11 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
             const int i = tid + NTH * j;
             if (bn < g.B && i < nd2) pfd[j] = d2g[(size_t)bn * nd2 + i];
         }
+        TRACE_PH(g, 2, 0, tph_);
         __syncthreads();
         float r[MAXT1Q];
         block2_rows(F2, T1, RS2, D2s, Qs, w2, w3, row_on, o, lane, r);
+        TRACE_PH(g, 2, 1, tph_);
         // BN3 (batch stats) -> ELU -> AvgPool(1,8) via 8-lane sums -> dropout -> h
         float xh[MAXT1Q], z[MAXT1Q];
 #pragma unroll
@@ -403,6 +439,7 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
             }
         }
         __syncthreads();
+        TRACE_PH(g, 2, 2, tph_);
         if (wave < NCLS) {                        // logits (model.py:78-82): wave n -> class n
             const int n = wave;
             float a = 0.f;
@@ -411,6 +448,7 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
             if (lane == 0) Ls[n] = a + prm[g.o_bfc + n];
         }
         __syncthreads();
+        TRACE_PH(g, 2, 3, tph_);
         if ((mode & PC_LOGITS) && tid < NCLS) logits[(size_t)b * NCLS + tid] = Ls[tid];
         if (mode & PC_BWD) {
             if (tid == 0) {
@@ -433,6 +471,7 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
                 for (int n = 0; n < NCLS; ++n) Ls[4 + n] = dl[n];
             }
             __syncthreads();
+            TRACE_PH(g, 2, 4, tph_);
             const float* DL = Ls + 4;
 #pragma unroll
             for (int i = 0; i < MAXW; ++i) {
@@ -447,6 +486,7 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
                 DP3s[i] = dh * keep_mul(g, mask3, 1, (size_t)b * NF + i);
             }
             __syncthreads();
+            TRACE_PH(g, 2, 5, tph_);
             if (row_on) {
 #pragma unroll
                 for (int m = 0; m < MAXT1Q; ++m) {
@@ -460,7 +500,9 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
             }
         }
         __syncthreads();
+        TRACE_PH(g, 2, 6, tph_);
     }
+    TRACE_LOOP(g, 2);
     if (mode & PC_BWD) {
         float* row = part + (size_t)blockIdx.x * g.nC;
 #pragma unroll
@@ -476,7 +518,7 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
         }
         if (tid == 0) pub(row + (NCLS * NF + NCLS + 2 * F2), lossacc);
         double* dsm = (double*)sm;
-        if (grid_reduce(g, part, g.nC, fa, dsm)) fin3(g, prm, dsm + 2, fa);
+        if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
     }
 }
 
@@ -496,6 +538,7 @@ __global__ __launch_bounds__(NTH) void k_pass_d(Geo g, const float* __restrict__
                                                 float* __restrict__ dp2g, float* __restrict__ part,
                                                 FinArgs fa) {
     EEG_DIMS(g);
+    TRACE(g, 3, TR_ENTRY);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2s = sm;
     float* Qs = D2s + F2 * RS2;        // q
@@ -535,6 +578,8 @@ __global__ __launch_bounds__(NTH) void k_pass_d(Geo g, const float* __restrict__
     }
     __syncthreads();
 
+    TRACE(g, 3, TR_PRO);
+    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -617,24 +662,31 @@ __global__ __launch_bounds__(NTH) void k_pass_d(Geo g, const float* __restrict__
         }
         __syncthreads();
     }
+    TRACE_LOOP(g, 3);
     float* row = part + (size_t)blockIdx.x * g.nD;
+    {
+        constexpr int NR = F2MAX + K2 + 4, NQ = NR / 4;   // [dW3 F2MAX][dw2 K2][sz][szx][pad 2]
+        float rv[NR];
 #pragma unroll
-    for (int i = 0; i < F2MAX; ++i) {
-        const float a = wave_sum(dW3p[i]);
-        if (row_on && lane == 0 && i < F2) pub(row + (o * F2 + i), a);
-    }
+        for (int i = 0; i < F2MAX; ++i) rv[i] = dW3p[i];
 #pragma unroll
-    for (int k = 0; k < K2; ++k) {
-        const float a = wave_sum(dw2p[k]);
-        if (row_on && lane == 0) pub(row + (F2 * F2 + o * K2 + k), a);
-    }
-    const float a = wave_sum(sz), ax = wave_sum(szx);
-    if (row_on && lane == 0) {
-        pub(row + (F2 * F2 + 16 * F2 + o), a);
-        pub(row + (F2 * F2 + 17 * F2 + o), ax);
+        for (int k = 0; k < K2; ++k) rv[F2MAX + k] = dw2p[k];
+        rv[F2MAX + K2] = sz; rv[F2MAX + K2 + 1] = szx; rv[F2MAX + K2 + 2] = 0.f; rv[F2MAX + K2 + 3] = 0.f;
+        wave_reduce<NR>(rv);
+        if (row_on && (lane & 15) == 0) {
+            const int r0 = (lane >> 4) * NQ;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                const int idx = j + r0;
+                if (idx < F2MAX) { if (idx < F2) pub(row + (o * F2 + idx), rv[j]); }
+                else if (idx < F2MAX + K2) pub(row + (F2 * F2 + o * K2 + idx - F2MAX), rv[j]);
+                else if (idx == F2MAX + K2) pub(row + (F2 * F2 + 16 * F2 + o), rv[j]);
+                else if (idx == F2MAX + K2 + 1) pub(row + (F2 * F2 + 17 * F2 + o), rv[j]);
+            }
+        }
     }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nD, fa, dsm)) fin4(g, prm, dsm + 2, fa);
+    if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
 }
 
 // ================================================================================================
@@ -649,6 +701,7 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
                                                 float* __restrict__ part, FinArgs fa) {
     using G_ = KG<K1>;
     EEG_DIMS(g);
+    TRACE(g, 4, TR_ENTRY);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     // x rows double-buffered when LDS allows (g.xdb): the next trial lands during phase B; otherwise
     // one buffer refilled after the dws GEMM, behind one extra barrier
@@ -689,20 +742,38 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
     const int kg0 = (NT16 * part_) / wpc, kg1 = gemm_on ? (NT16 * (part_ + 1)) / wpc : 0;
     floatx4 xacc = {0.f, 0.f, 0.f, 0.f};
     float pf[PF];
-    if ((int)blockIdx.x < g.B) x_prefetch<PF>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
+    // dp2 rows of the next trial ride along with its x (one trial ahead, registers): a synchronous
+    // load here would wait (vmcnt is in order) for the whole x prefetch issued before it
+    constexpr int NDP = (CC && TT) ? (FF * (TT / 4) + NTH - 1) / NTH : 4;   // F2 * T1 <= NDP * NTH
+    const int ndp = F2 * T1;
+    float pdp[NDP];
+    if ((int)blockIdx.x < g.B) {
+        x_prefetch<PF>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
+        for (int i = tid; i < ndp; i += NTH) DP[i] = dp2g[(size_t)blockIdx.x * ndp + i];
+    }
     __syncthreads();
     x_store<PF>(pf, C, T, RS, LP, Xb0, tid);
     __syncthreads();
 
     int it = 0;
+    TRACE(g, 4, TR_PRO);
+    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = (it & 1) ? Xb1 : Xb0;
         float* Xn = (it & 1) ? Xb0 : Xb1;
         const int bn = b + gridDim.x;
-        if (bn < g.B) x_prefetch<PF>(x + (size_t)bn * C * T, C, T, pf, tid);
-        for (int i = tid; i < F2 * T1; i += NTH) DP[i] = dp2g[(size_t)b * F2 * T1 + i];
+        if (bn < g.B) {
+            x_prefetch<PF>(x + (size_t)bn * C * T, C, T, pf, tid);
+#pragma unroll
+            for (int j = 0; j < NDP; ++j) {
+                const int i = tid + NTH * j;
+                if (i < ndp) pdp[j] = dp2g[(size_t)bn * ndp + i];
+            }
+        }
         spatial_mfma<KS>(Xc, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+        TRACE_PH(g, 4, 0, tph_);
         __syncthreads();                                   // Ss, DP complete
+        TRACE_PH(g, 4, 1, tph_);
         if (row_on) {
             const float* row = Ss + o * RS;
             float* drow = Dys + o * RS + LP;
@@ -734,6 +805,7 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
                 }
                 lds_st4(drow + 4 * q, (floatx4){dy[0], dy[1], dy[2], dy[3]});
             }
+            TRACE_PH(g, 4, 2, tph_);
             wave_lds_fence();
             // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
             const float* dyr = Dys + o * RS;
@@ -752,8 +824,11 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
                 lds_st4(erow + 4 * q, (floatx4){e[0], e[1], e[2], e[3]});
             }
         }
+        TRACE_PH(g, 4, 3, tph_);
         if (xdb && bn < g.B) x_store<PF>(pf, C, T, RS, LP, Xn, tid);
+        TRACE_PH(g, 4, 4, tph_);
         __syncthreads();                                   // e rows complete, Xn staged
+        TRACE_PH(g, 4, 5, tph_);
         // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
         // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
         if (gemm_on) {
@@ -772,26 +847,42 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
                 xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
             }
         }
+        if (bn < g.B) {                            // next trial's dp2 rows: every FIR reader is past
+#pragma unroll
+            for (int j = 0; j < NDP; ++j) {
+                const int i = tid + NTH * j;
+                if (i < ndp) DP[i] = pdp[j];
+            }
+        }
+        TRACE_PH(g, 4, 6, tph_);
         __syncthreads();                                   // e rows consumed before the next s
+        TRACE_PH(g, 4, 7, tph_);
         if (!xdb && bn < g.B) {
             x_store<PF>(pf, C, T, RS, LP, Xn, tid);
             __syncthreads();
         }
     }
+    TRACE_LOOP(g, 4);
     __syncthreads();
 
     // ---- reductions ----
     float* row = part + (size_t)blockIdx.x * g.nE;
-#pragma unroll
-    for (int k = 0; k < K1; ++k) {
-        const float a = wave_sum(Q[k]);
-        if (row_on && lane == 0) pub(row + (o * K1 + k), a);
-    }
     {
-        const float a = wave_sum(sdy), a2 = wave_sum(sdyv);
-        if (row_on && lane == 0) {
-            pub(row + (F2 * K1 + F2 * C + o), a);
-            pub(row + (F2 * K1 + F2 * C + F2 + o), a2);
+        constexpr int NR = K1 + 4, NQ = NR / 4;         // [Q K1][sdy][sdyv][pad 2]
+        float rv[NR];
+#pragma unroll
+        for (int k = 0; k < K1; ++k) rv[k] = Q[k];
+        rv[K1] = sdy; rv[K1 + 1] = sdyv; rv[K1 + 2] = 0.f; rv[K1 + 3] = 0.f;
+        wave_reduce<NR>(rv);
+        if (row_on && (lane & 15) == 0) {
+            const int r0 = (lane >> 4) * NQ;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                const int idx = j + r0;
+                if (idx < K1) pub(row + (o * K1 + idx), rv[j]);
+                else if (idx == K1) pub(row + (F2 * K1 + F2 * C + o), rv[j]);
+                else if (idx == K1 + 1) pub(row + (F2 * K1 + F2 * C + F2 + o), rv[j]);
+            }
         }
     }
     // Xm: wave -> 16x16 tile partial (rows 4lk+r, col li) -> LDS [wave][256] -> sum over the
@@ -807,7 +898,7 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
         pub(row + (F2 * K1 + p), a);
     }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nE, fa, dsm)) fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa);
+    if (grid_reduce(g, part, g.nE, fa, dsm)) { fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa); TRACE(g, 4, TR_FIN); }
 }
 
 // ================================================================================================
@@ -820,6 +911,7 @@ __global__ __launch_bounds__(NTH) void k_infer(Geo g, const float* __restrict__ 
                                                const float* __restrict__ x, float* __restrict__ logits) {
     using G_ = KG<K1>;
     EEG_DIMS(g);
+    TRACE(g, 5, TR_ENTRY);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* const Xb0 = sm;             // one x buffer: the next trial lands after its last reader
     float* Ss = sm + C * RS;
@@ -866,6 +958,8 @@ __global__ __launch_bounds__(NTH) void k_infer(Geo g, const float* __restrict__ 
     __syncthreads();
 
     int it = 0;
+    TRACE(g, 5, TR_PRO);
+    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = Xb0;
         float* Xn = Xb0;

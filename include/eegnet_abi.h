@@ -113,6 +113,13 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
 int eegnet_profile_enable(int on);
 int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, int* n_out);
 
+/* Optional timeline instrumentation for kernel tuning: while `buf` (a zeroed device buffer of
+ * eegnet_trace_bytes() bytes) is set, every pass kernel stamps phase boundaries into it
+ * ([pass][workgroup][16] uint64: wall clock at entry / prologue / loop end / publish / tickets /
+ * finalize, shader-clock sums of in-loop phases).  NULL turns it off. */
+int eegnet_trace_enable(void* buf);
+size_t eegnet_trace_bytes(void);
+
 /* Thread-local description of the last error ("" if none). */
 const char* eegnet_last_error(void);
 

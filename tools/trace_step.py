@@ -1,0 +1,82 @@
+"""Timeline of one EEGNet train step from the kernels' own stamps (eegnet_trace_enable).
+
+    python tools/trace_step.py [--batch B]
+
+Per pass: launch skew, prologue, trial loop, publish, group/top reduction, finalize (µs, wall clock
+at 100 MHz), the gap to the next kernel, and the shader-clock in-loop phase sums per trial.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("EEGNET_LIB", "libeegnet_hip_trace.so")
+sys.path.insert(0, ROOT)
+
+NAMES = ["A", "B", "C", "D", "E", "infer"]
+SLOTS, MAXWG = 16, 2048
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--C", type=int, default=22)
+    ap.add_argument("--T", type=int, default=256)
+    args = ap.parse_args()
+    from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = EEGNet(args.C, args.T, p=0.5).to(dev).train()
+    rng = np.random.default_rng(1234)
+    x = torch.from_numpy(rng.standard_normal((args.batch, args.C, args.T), dtype=np.float32)).to(dev)
+    y = torch.from_numpy(rng.integers(0, 4, args.batch)).to(dev)
+    tr = FusedTrainer(model)
+    for _ in range(5):
+        tr.step(x, y)
+    nb = lib.eegnet_trace_bytes()
+    buf = torch.zeros(nb // 8, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    lib.eegnet_trace_enable(ctypes.c_void_p(buf.data_ptr()))
+    tr.step(x, y)
+    torch.cuda.synchronize()
+    lib.eegnet_trace_enable(None)
+    a = buf.cpu().numpy().reshape(8, MAXWG, SLOTS).astype(np.float64)
+    grid = int((a[0, :, 0] > 0).sum())
+    t0 = a[0, :grid, 0].min()
+    us = lambda v: (v - t0) / 100.0   # 100 MHz wall clock -> µs from pass A's first entry
+    prev_end = None
+    ntr = max(1, args.batch // grid)
+    print(f"grid={grid} workgroups, {ntr} trials per workgroup")
+    for p in range(5):
+        st = a[p, :grid]
+        ent, pro, loop, pub = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
+        grp = st[:, 4][st[:, 4] > 0]
+        top = st[:, 5][st[:, 5] > 0]
+        fin = st[:, 6][st[:, 6] > 0]
+        end = max(v.max() for v in (pub, grp, top, fin) if len(v))
+        line = (f"pass {NAMES[p]}: start {us(ent.min()):7.1f} (skew {(ent.max()-ent.min())/100:5.1f})"
+                f" | prologue {np.mean(pro-ent)/100:5.1f} | loop avg {np.mean(loop-pro)/100:6.1f} max {np.max(loop-pro)/100:6.1f}"
+                f" | publish {np.mean(pub-loop)/100:5.1f} | last pub {us(pub.max()):7.1f}")
+        if len(grp):
+            line += f" | grp-red {(grp.max()-pub.max())/100:5.1f}"
+        if len(top):
+            line += f" | top {(top.max()-grp.max())/100:5.1f}"
+        if len(fin):
+            line += f" | fin {(fin.max()-top.max())/100:5.1f}"
+        line += f" | end {us(end):7.1f}"
+        if prev_end is not None:
+            line += f" | gap {(ent.min()-prev_end)/100:5.1f}"
+        prev_end = end
+        print(line)
+        ph = st[:, 8:16].mean(axis=0) / ntr
+        if ph.any():
+            print("    in-loop phases (shader cycles per trial, wave 0):", " ".join(f"{v:.0f}" for v in ph))
+
+
+if __name__ == "__main__":
+    main()
