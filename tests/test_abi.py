@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _header_symbols():
     txt = open(os.path.join(ROOT, "include", "eegnet_abi.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(eegnet_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(eegnet_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_matches_binding():
