@@ -40,6 +40,8 @@ struct Geo {
     int LP, RS;          // x / s / dy / e rows in LDS: left pad, row stride (floats, RS/4 odd)
     int TQ, NT16;        // ceil(T/4) quads, ceil(T/16) MFMA column tiles
     int RS2;             // block_2 rows (d2 / q / dq) stride
+    int RSW;             // per-wave block-2 rows of passes C / D (row_stride_b2)
+    int nwC, nwD;        // trial streams (waves) per workgroup of passes C / D
     int CK, NCT, NKG;    // C padded to 4, ceil(C/16), ceil(T/16) k-groups of the dws GEMM
     int nH, nTl, nedge;  // lag-Gram edge terms: head pairs R(R+1)/2, tail pairs P(P+1)/2, + R + P sums
     float p, scale, eps, mom;
@@ -47,6 +49,8 @@ struct Geo {
     int xdb;             // pass E: double-buffered x rows
     int noclamp;         // skip the model.py:44/84 clamps (data-parallel: clamp after all-reduce)
     unsigned long long key;
+    unsigned key0, key1;  // per-layer 32-bit dropout keys (derived from key)
+    unsigned pthr;        // dropout threshold p * 2^24
     // flat parameter offsets (named_parameters order)
     int o_w1, o_g1, o_b1, o_ws, o_g2, o_b2, o_w2, o_W3, o_g3, o_b3, o_Wfc, o_bfc, nparam;
     // partial-row lengths of the five passes and the (common) workgroup count
@@ -77,18 +81,29 @@ enum TraceEv { TR_ENTRY = 0, TR_PRO, TR_LOOP, TR_PUB, TR_GRP, TR_TOP, TR_FIN, TR
     do {                                                                                         \
         if (TRACE_ON(g_) && threadIdx.x == 0) {                                                  \
             const unsigned long long t1_ = clock64();                                            \
-            tacc_[ph_] += t1_ - (t0_);                                                           \
+            tr_lds_[ph_] += t1_ - (t0_);                                                         \
             (t0_) = t1_;                                                                         \
         }                                                                                        \
     } while (0)
-// loop-end stamp plus the register-held phase sums
+// loop-end stamp plus the phase sums (kept in a static LDS slot, not registers: tracing must not
+// change the register allocation of the kernel it measures)
 #define TRACE_LOOP(g_, pass_)                                                                    \
     do {                                                                                         \
         TRACE(g_, pass_, TR_LOOP);                                                               \
         if (TRACE_ON(g_) && threadIdx.x == 0)                                                    \
             for (int ph_ = 0; ph_ < 8; ++ph_)                                                    \
-                (g_).trace[((size_t)(pass_) * TR_MAXWG + blockIdx.x) * TR_SLOTS + TR_PH0 + ph_] = tacc_[ph_]; \
+                (g_).trace[((size_t)(pass_) * TR_MAXWG + blockIdx.x) * TR_SLOTS + TR_PH0 + ph_] = tr_lds_[ph_]; \
     } while (0)
+#ifdef EEGNET_TRACE
+#define TRACE_DECL()                                                                             \
+    __shared__ unsigned long long tr_lds_[8];                                                    \
+    if (threadIdx.x == 0)                                                                        \
+        for (int ph_ = 0; ph_ < 8; ++ph_) tr_lds_[ph_] = 0;                                      \
+    unsigned long long tph_ = clock64();                                                         \
+    (void)tph_
+#else
+#define TRACE_DECL() unsigned long long tph_ = 0; unsigned long long* tr_lds_ = nullptr; (void)tph_; (void)tr_lds_
+#endif
 
 // coefficient block layout (float, CSTR per field; F1, F2 <= 64)
 enum CoefField {
@@ -135,6 +150,12 @@ __host__ __device__ constexpr int row_stride(int K1, int T) {
     return ((rs / 4) & 1) ? rs : rs + 4;
 }
 __host__ __device__ constexpr int row_stride2(int T) { return rup4(LP2 + T / 4 + 8); }
+// per-wave block-2 rows of passes C / D (T1 = T/4 pooled samples): pads of 7 / 8 on the left and
+// room for the last 16-column MFMA group; RSW/4 odd so 16 rows read as float4 columns hit distinct banks
+__host__ __device__ constexpr int row_stride_b2(int T1) {
+    const int r = rup4(T1 + 24);
+    return ((r / 4) & 1) ? r : r + 4;
+}
 
 // compile-time row geometry for a temporal kernel length
 template <int K1>
@@ -155,17 +176,42 @@ __device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : expm1f(z)
 __device__ __forceinline__ float elu_d(float z) { return z > 0.f ? 1.f : expf(z); }
 
 // Dropout keep factor (model.py:50,74 nn.Dropout: x * mask / (1-p)).  Injected masks win; otherwise a
-// counter-based splitmix64 draw keyed by (key, layer, flat index) -- identical in forward and backward.
+// counter-based draw: murmur3's 32-bit finalizer of (flat index * golden ratio + per-layer key), top
+// 24 bits against p * 2^24.  Identical in forward and backward, a few VALU ops per element.
 __device__ __forceinline__ float keep_mul(const Geo& g, const uint8_t* __restrict__ mask, int layer,
-                                          unsigned long long idx) {
+                                          unsigned idx) {
     if (!g.drop) return 1.f;
     if (mask) return mask[idx] ? g.scale : 0.f;
-    unsigned long long z = g.key + ((unsigned long long)(layer + 1) << 56) + idx * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    const float u = (float)(unsigned)(z >> 40) * (1.0f / 16777216.0f);
-    return u >= g.p ? g.scale : 0.f;
+    unsigned h = idx * 0x9E3779B1u + (layer ? g.key1 : g.key0);
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return (h >> 8) >= g.pthr ? g.scale : 0.f;
+}
+
+// Drain every outstanding memory operation before a trial loop.  The waitcnt pass merges the
+// pre-loop state of register-resident operands (MFMA A fragments, taps) into the loop header and
+// then guards their first in-loop use with vmcnt waits -- which, vmcnt being in order, also wait for
+// the NEXT trial's x prefetch issued at the top of the iteration.  One explicit drain here resolves
+// those operands for good.
+__device__ __forceinline__ void drain_prologue_loads() { __builtin_amdgcn_s_waitcnt(0); }
+
+// a wave-uniform zero the compiler cannot see through: added to a weight-row offset it pins that
+// row's scalar loads next to their use (otherwise every row of every table is hoisted into SGPRs and
+// spilled)
+__device__ __forceinline__ int opaque0() {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+// the same, ordered after `dep` is computed: chains row r's weight loads behind row r-1's result so
+// the compiler cannot hoist every row's loads to the top (asm volatile alone may all move up)
+__device__ __forceinline__ int opaque0_after(float dep) {
+    int z = 0;
+    asm volatile("" : "+s"(z) : "v"(dep));
+    return z;
 }
 
 // ---- cross-lane reductions: v_permlane32/16_swap halving + DPP within 16-lane rows ----
@@ -334,6 +380,28 @@ __device__ __forceinline__ void spatial_mfma(const float* Xs, const float (&aw)[
         for (int r = 0; r < 4; ++r) {
             const int o = 4 * lk + r;
             if (o < F2) Ss[o * RS + LP + 16 * n + li] = acc[r];
+        }
+    }
+}
+
+// Lag correlation on the matrix cores.  sum_t a[t] b[t+k-P] (k < K1) = sum_i M[i][i+k] with the
+// row-block matrix M[i][m] = sum_j a[16j+i] b[16j+m-P], m < 16*NTQ, accumulated in NTQ 16x16x4 f32
+// tiles (exact f32 fmaf chains).  Lane l: A[i = l&15][j = 4s + (l>>4)], B[j][m = 16nt + (l&15)];
+// D[4(l>>4)+r][16nt + (l&15)].  a: LDS row at t = 0, zero for t in [T, 16 NJ); b: LDS row at t = 0
+// with >= P zeros on the left; reads of b at t >= T are masked to zero.
+template <int NTQ>
+__device__ __forceinline__ void lagcorr_mfma(const float* a, const float* b, int T, int NJ, int P,
+                                             floatx4 (&acc)[NTQ], int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+    for (int s = 0; 4 * s < NJ; ++s) {
+        const int j = 4 * s + lk;
+        const bool jon = j < NJ;
+        const float av = jon ? a[16 * j + li] : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NTQ; ++nt) {
+            const int tb = 16 * j + 16 * nt + li - P;
+            const float bv = (jon && tb < T) ? b[tb] : 0.f;
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[nt], 0, 0, 0);
         }
     }
 }

@@ -59,8 +59,8 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     TRACE(g, tp, TR_PUB);
     if (!take_ticket(fa.cnt + grp, (unsigned)nr, flag)) return false;
     // group reducer: rows [r0, r1), rs interleaved row subsets per column, then the rs-way sum
-    const int rs = max(1, min(nr, NTH / ncols));
-    for (int idx = tid; idx < rs * ncols; idx += NTH) {
+    const int rs = max(1, min(nr, (int)blockDim.x / ncols));
+    for (int idx = tid; idx < rs * ncols; idx += (int)blockDim.x) {
         const int sub = idx / ncols, c = idx - sub * ncols;
         const float* col = part + c;
         double a = 0.0;
@@ -76,14 +76,14 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
         scr[idx] = a;
     }
     __syncthreads();
-    for (int c = tid; c < ncols; c += NTH) {
+    for (int c = tid; c < ncols; c += (int)blockDim.x) {
         double a = 0.0;
         for (int sub = 0; sub < rs; ++sub) a += scr[sub * ncols + c];
         pub(fa.part2 + (size_t)grp * ncols + c, a);
     }
     TRACE(g, tp, TR_GRP);
     if (!take_ticket(fa.cnt + (NCNT - 1), (unsigned)g.ngrp, flag)) return false;
-    for (int c = tid; c < ncols; c += NTH) {
+    for (int c = tid; c < ncols; c += (int)blockDim.x) {
         double v[NGRPMAX];
 #pragma unroll
         for (int q = 0; q < NGRPMAX; ++q) v[q] = q < g.ngrp ? fa.part2[(size_t)q * ncols + c] : 0.0;
@@ -101,7 +101,7 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
 }
 
 // ================================================================================================
-// Finalize bodies (run by the last workgroup of each pass, NTH threads): BN constants, running
+// Finalize bodies (run by the last workgroup of each pass, blockDim.x threads): BN constants, running
 // statistics, parameter gradients, clamps; Adam after pass E.
 // ================================================================================================
 __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, double var, double n,
@@ -159,11 +159,11 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
             if (k < K1 - 1) acc += (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
         }
     }
-    for (int i = tid; i < F1 * K1; i += NTH) wd[i] = (double)prm[g.o_w1 + i];
+    for (int i = tid; i < F1 * K1; i += (int)blockDim.x) wd[i] = (double)prm[g.o_w1 + i];
     __syncthreads();
-    for (int i = tid; i < K1 * K1 + K1; i += NTH) fa.stats[i] = Gm[i];
+    for (int i = tid; i < K1 * K1 + K1; i += (int)blockDim.x) fa.stats[i] = Gm[i];
     // quadratic forms w^T G w and w^T S1, one (filter, tap) per thread (G symmetric: column reads)
-    for (int p = tid; p < F1 * K1; p += NTH) {
+    for (int p = tid; p < F1 * K1; p += (int)blockDim.x) {
         const int gg = p / K1, k = p - gg * K1;
         const double* w = wd + gg * K1;
         double r = 0.0;
@@ -226,7 +226,7 @@ __device__ void fin2(const Geo& g, const double* sums, const FinArgs& fa) {
 __device__ void fin3(const Geo& g, const float* prm, const double* sums, const FinArgs& fa) {
     const int tid = threadIdx.x;
     const int n4 = NCLS * g.NF;
-    for (int p = tid; p < n4; p += NTH) {
+    for (int p = tid; p < n4; p += (int)blockDim.x) {
         const float v = (float)sums[p];
         fa.grads[g.o_Wfc + p] = g.noclamp ? v : fminf(fmaxf(v, -0.25f), 0.25f);
     }
@@ -252,8 +252,8 @@ __device__ void fin3(const Geo& g, const float* prm, const double* sums, const F
 // after pass D: block_2 grads, BN2 grads and the dy2 constants
 __device__ void fin4(const Geo& g, const float* prm, const double* sums, const FinArgs& fa) {
     const int tid = threadIdx.x;
-    for (int p = tid; p < g.F2 * g.F2; p += NTH) fa.grads[g.o_W3 + p] = (float)sums[p];
-    for (int p = tid; p < g.F2 * 16; p += NTH) fa.grads[g.o_w2 + p] = (float)sums[g.F2 * g.F2 + p];
+    for (int p = tid; p < g.F2 * g.F2; p += (int)blockDim.x) fa.grads[g.o_W3 + p] = (float)sums[p];
+    for (int p = tid; p < g.F2 * 16; p += (int)blockDim.x) fa.grads[g.o_w2 + p] = (float)sums[g.F2 * g.F2 + p];
     if (tid < g.F2) {
         const int o = tid;
         const double sdz = sums[g.F2 * g.F2 + 16 * g.F2 + o];
@@ -291,9 +291,9 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     const double* Xm = sums + g.F2 * K1;
     const double* Sdy = Xm + g.F2 * g.C;
     const double* Sdyv = Sdy + g.F2;
-    for (int i = tid; i < K1 * K1 + K1; i += NTH) Gm[i] = fa.stats[i];
-    for (int i = tid; i < F1 * K1; i += NTH) wd[i] = (double)prm[g.o_w1 + i];
-    for (int p = tid; p < g.F2 * g.C; p += NTH) {
+    for (int i = tid; i < K1 * K1 + K1; i += (int)blockDim.x) Gm[i] = fa.stats[i];
+    for (int i = tid; i < F1 * K1; i += (int)blockDim.x) wd[i] = (double)prm[g.o_w1 + i];
+    for (int p = tid; p < g.F2 * g.C; p += (int)blockDim.x) {
         const int o = p / g.C, gg = o / g.D;
         const double v = (double)fa.coef[CF_A1 * CSTR + gg] * Xm[p] + (double)fa.coef[CF_C1 * CSTR + gg] * Sdy[o];
         fa.grads[g.o_ws + p] = g.noclamp ? (float)v : fminf(fmaxf((float)v, -1.0f), 1.0f);
@@ -313,7 +313,7 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     }
     __syncthreads();
     const double n1 = (double)g.B * g.C * g.T;
-    for (int p = tid; p < F1 * K1; p += NTH) {
+    for (int p = tid; p < F1 * K1; p += (int)blockDim.x) {
         const int gg = p / K1, k = p - gg * K1;
         const double* w = wd + gg * K1;
         double qg = 0.0;
@@ -331,7 +331,7 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     const int s = *fa.step + 1;
     const float step_size = (float)((double)fa.lr / (1.0 - pow((double)fa.b1, (double)s)));
     const float bc2s = (float)sqrt(1.0 - pow((double)fa.b2, (double)s));
-    for (int i = tid; i < g.nparam; i += NTH)
+    for (int i = tid; i < g.nparam; i += (int)blockDim.x)
         adam_elem(fa.params + i, fa.grads[i], fa.adam_m + i, fa.adam_v + i, fa.b1, fa.b2, step_size,
                   bc2s, fa.eps);
     __syncthreads();

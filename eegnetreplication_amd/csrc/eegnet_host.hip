@@ -17,6 +17,9 @@ static int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+// dynamic LDS per workgroup: 160 KiB less a little room for the static LDS of the traced build
+constexpr int LDS_MAX = 160 * 1024 - 256;
+
 static inline int rup(int a, int m) { return (a + m - 1) / m * m; }
 static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
 
@@ -112,11 +115,17 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     const int nf4 = rup(g->NF, 4);
     g->ldsA = rows1 + g->F2 * g->RS + NWAVE * (g->K1 + 1);
     g->ldsB = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2;
-    g->ldsC = 2 * g->F2 * g->RS2 + 2 * nf4 + 8;
-    g->ldsD = 4 * g->F2 * g->RS2 + nf4;
+    // passes C / D: one trial stream per wave, each with its own block-2 rows (row_stride_b2)
+    g->RSW = row_stride_b2(g->T1);
+    const int pwC = nf4, pwD = 3 * g->F2 * g->RSW + nf4;
+    const bool spec = g->C == 22 && (g->T == 256 || g->T == 257) && g->F2 == 16 && g->K1 == 32;   // EEG_DISPATCH
+    g->nwC = std::max(1, std::min(spec ? NWAVE : NTHS / 64, (LDS_MAX / 4) / pwC));
+    g->nwD = std::max(1, std::min(NTHS / 64, (LDS_MAX / 4) / pwD));
+    g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);
+    g->ldsD = std::max(g->nwD * pwD, g->nwD * g->nD);
     g->ldsE = 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4);
-    g->xdb = (wg_per_cu() == 1 && (g->ldsE + rows2) * 4 <= 160 * 1024) ? 1 : 0;
-    g->ldsE = std::max(g->ldsE + (g->xdb ? rows2 : rows1), NWAVE * 256);
+    g->xdb = (wg_per_cu() == 1 && (g->ldsE + rows2) * 4 <= LDS_MAX) ? 1 : 0;
+    g->ldsE = std::max(g->ldsE + (g->xdb ? rows2 : rows1), NWAVE * 256 + NWAVE * 16 * (g->K1 + 16));   // + lag tiles
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
     auto tail = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + std::max(tail_scratch_doubles(ncols), fin)); };
@@ -134,10 +143,12 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
                         NTH * MAXPF);
         if (g->T1 > 64 * MAXT1Q) return fail(EEGNET_EINVAL, "T/4 > %d", 64 * MAXT1Q);
         if (g->F2 * g->T1 > 4 * NTH) return fail(EEGNET_EINVAL, "F2*(T/4) > %d", 4 * NTH);
-        if (NCLS * g->NF > 4 * NTH) return fail(EEGNET_EINVAL, "F2*(T/32) too large");
+        if ((double)g->B * g->F2 * g->T1 >= 4294967296.0)
+            return fail(EEGNET_EINVAL, "B*F2*(T/4) must stay below 2^32 (dropout / mask indices)");
+        if (g->NF > 64 * MAXNFQ) return fail(EEGNET_EINVAL, "F2*(T/32) = %d > %d", g->NF, 64 * MAXNFQ);
         const int lmax = std::max(std::max(std::max(g->ldsA, g->ldsB), std::max(g->ldsC, g->ldsD)),
                                   std::max(g->ldsE, g->ldsI));
-        if (lmax * 4 > 160 * 1024) return fail(EEGNET_EINVAL, "dims need %d B of LDS (> 160 KiB)", lmax * 4);
+        if (lmax * 4 > LDS_MAX) return fail(EEGNET_EINVAL, "dims need %d B of LDS (> %d)", lmax * 4, LDS_MAX);
     }
     return 0;
 }
@@ -168,6 +179,14 @@ static uint64_t mix_key(uint64_t seed, uint64_t offset) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+// dropout keys of one call: (seed, offset) -> 64-bit key -> two per-layer 32-bit keys, threshold
+static void set_key(Geo* g, uint64_t seed, uint64_t offset) {
+    g->key = mix_key(seed, offset);
+    g->key0 = (unsigned)g->key;
+    g->key1 = (unsigned)(g->key >> 32) ^ 0x5BD1E995u;
+    g->pthr = (unsigned)std::min(16777216.0, std::max(0.0, (double)g->p * 16777216.0));
 }
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
@@ -205,7 +224,7 @@ static bool g_attr_done = false;
 
 template <int K1, int CC, int TT, int FF>
 static void set_attrs_shape() {
-    const int lds = 160 * 1024;
+    const int lds = LDS_MAX;
     hipFuncSetAttribute((const void*)k_pass_a<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipFuncSetAttribute((const void*)k_pass_b<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipFuncSetAttribute((const void*)k_pass_c<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -287,12 +306,12 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
         fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
     }
-#define LAUNCH_CB(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsC * 4, s, \
+#define LAUNCH_CB(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwC), g.ldsC * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
                        (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fc)
     { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
     } LAUNCH_CHECK("k_pass_c(bwd)");
-#define LAUNCH_D(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsD * 4, s, \
+#define LAUNCH_D(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
                        (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2), \
                        (float*)(ws + L.partD), fd)
@@ -338,7 +357,7 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     if (int r = check_ptrs(x, "x", logits, "logits")) return r;
     if (int r = check_ptrs(ws, "ws")) return r;
     g.drop = g.p > 0.f ? 1 : 0;
-    g.key = mix_key(seed, offset);
+    set_key(&g, seed, offset);
     ensure_attrs();
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;
@@ -349,7 +368,7 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     if (r) return r;
     FinArgs none;
     memset(&none, 0, sizeof(none));
-#define LAUNCH_CF(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsC * 4, s, \
+#define LAUNCH_CF(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwC), g.ldsC * 4, s, \
                        g, params, (const float*)(w + L.coef), (const float*)(w + L.d2), mask3, (const float*)nullptr, \
                        (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS, none)
     { PROF(KID_C);
@@ -369,7 +388,7 @@ int eegnet_backward(const eegnet_dims* dims, const float* params, const float* x
     if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
     if (!dlogits && !labels) return fail(EEGNET_EINVAL, "need dlogits or labels");
     g.drop = g.p > 0.f ? 1 : 0;
-    g.key = mix_key(seed, offset);
+    set_key(&g, seed, offset);
     ensure_attrs();
     const WsLayout L = make_layout(g);
     const int mode = PC_BWD | (dlogits ? 0 : PC_CE);
@@ -423,7 +442,7 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     if (adam_state && !step) return fail(EEGNET_EINVAL, "step is NULL");
     g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
     g.drop = g.p > 0.f ? 1 : 0;
-    g.key = mix_key(seed, offset);
+    set_key(&g, seed, offset);
     ensure_attrs();
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;

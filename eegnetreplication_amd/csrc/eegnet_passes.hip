@@ -82,7 +82,8 @@ __global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__
 
     int it = 0;
     TRACE(g, 0, TR_PRO);
-    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
+    TRACE_DECL();
+    drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = Xb0;
         float* Xn = Xb0;
@@ -235,7 +236,8 @@ __global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__
 
     int it = 0;
     TRACE(g, 1, TR_PRO);
-    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
+    TRACE_DECL();
+    drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = Xb0;
         float* Xn = Xb0;
@@ -351,11 +353,161 @@ __device__ __forceinline__ void block2_rows(int F2, int T1, int RS2, const float
 }
 
 // ================================================================================================
-// Pass C: head (model.py:71-84).  logits, and (PC_BWD) classifier grads + BN3 backward sums.
+// Block-2-rate passes C and D: one trial per wave.  Lane t holds pooled sample t (+64 m) of all F2
+// rows, so block_2's pointwise mix, BN3, ELU and the backward elementwise chain are lane-local
+// register work with wave-uniform (scalar) weights, and the two depthwise 1x16 convolutions take
+// their neighbours from DPP lane shifts (wave_shr / wave_shl).  No workgroup barrier inside the
+// trial loop: the waves of a workgroup are independent trial streams until the final reduction.
+// ================================================================================================
+constexpr int NTHS = 512;       // workgroup bound of pass D and of the runtime-shape pass C
+constexpr int LPQ = 8;          // left pad of pass D's LDS rows (16-byte aligned MFMA / window reads)
+constexpr int LPD = 7;          // left pad of pass D's d2 rows: d2p[t + k - 7] sits at [t + k]
+constexpr int MAXNFQ = 8;       // flattened head features per lane: F2*(T/32) <= 512
+
+// 8-lane sums of consecutive lanes: after the three DPP steps lanes 8i+4..8i+7 hold the sum of
+// lanes 8i..8i+7 (quad sums, then row_shr:4 adds the neighbouring quad; bound_ctrl zero-fills)
+__device__ __forceinline__ float sum8_hi(float v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xF, 0xF, true));
+    return v;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// x[t] <- x[t-1] / x[t+1] over the row t = lane + 64 m, zero shifted in at the ends
+template <int MQ>
+__device__ __forceinline__ void shr1(float (&x)[MQ], int lane) {
+#pragma unroll
+    for (int m = MQ - 1; m >= 0; --m) {
+        const float carry = m > 0 ? readlane_f(x[m > 0 ? m - 1 : 0], 63) : 0.f;
+        const float v = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x[m]), 0x138, 0xF, 0xF, true));
+        x[m] = (m > 0 && lane == 0) ? carry : v;
+    }
+}
+template <int MQ>
+__device__ __forceinline__ void shl1(float (&x)[MQ], int lane) {
+#pragma unroll
+    for (int m = 0; m < MQ; ++m) {
+        const float carry = m < MQ - 1 ? readlane_f(x[m < MQ - 1 ? m + 1 : m], 0) : 0.f;
+        const float v = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x[m]), 0x130, 0xF, 0xF, true));
+        x[m] = (m < MQ - 1 && lane == 63) ? carry : v;
+    }
+}
+
+// y[t] = sum_k w[k] x[t + k - 7]: depthwise 1x16 'same' conv (model.py:54-61, pad 7 | 8); x is
+// zero outside [0, T1)
+template <int MQ>
+__device__ __forceinline__ void conv16_same(const float (&x)[MQ], const float* __restrict__ w, float (&y)[MQ],
+                                            int lane) {
+    float s[MQ];
+#pragma unroll
+    for (int m = 0; m < MQ; ++m) { y[m] = w[7] * x[m]; s[m] = x[m]; }
+#pragma unroll
+    for (int k = 6; k >= 0; --k) {                 // s = x[t - (7 - k)]
+        shr1<MQ>(s, lane);
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) y[m] = fmaf(w[k], s[m], y[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < MQ; ++m) s[m] = x[m];
+#pragma unroll
+    for (int k = 8; k < K2; ++k) {                 // s = x[t + k - 7]
+        shl1<MQ>(s, lane);
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) y[m] = fmaf(w[k], s[m], y[m]);
+    }
+}
+
+// its transpose: y[t] = sum_k w[k] x[t + 7 - k] (the input gradient of conv16_same)
+template <int MQ>
+__device__ __forceinline__ void conv16_same_t(const float (&x)[MQ], const float* __restrict__ w, float (&y)[MQ],
+                                              int lane) {
+    float s[MQ];
+#pragma unroll
+    for (int m = 0; m < MQ; ++m) { y[m] = w[7] * x[m]; s[m] = x[m]; }
+#pragma unroll
+    for (int k = 6; k >= 0; --k) {                 // s = x[t + 7 - k]
+        shl1<MQ>(s, lane);
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) y[m] = fmaf(w[k], s[m], y[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < MQ; ++m) s[m] = x[m];
+#pragma unroll
+    for (int k = 8; k < K2; ++k) {                 // s = x[t - (k - 7)]
+        shr1<MQ>(s, lane);
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) y[m] = fmaf(w[k], s[m], y[m]);
+    }
+}
+
+// d2 rows of trial b into registers (lane t, chunk m); zero beyond T1.  Wave-uniform row base:
+// saddr + 32-bit lane offset loads.
+template <int MQ>
+__device__ __forceinline__ void load_rows(const float* __restrict__ src, int b, int F2, int T1, int lane,
+                                          float (&d)[F2MAX][MQ]) {
+    const float* base = src + (size_t)b * F2 * T1;
+#pragma unroll
+    for (int o = 0; o < F2MAX; ++o)
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) {
+            const int t = lane + 64 * m;
+            d[o][m] = (o < F2 && t < T1) ? base[o * T1 + t] : 0.f;
+        }
+}
+
+// q = conv16_same of every d2 row, each row's taps scalar-loaded next to their use
+template <int MQ>
+__device__ __forceinline__ void dwconv_rows(const Geo& g, const float* __restrict__ prm, int F2,
+                                            const float (&d)[F2MAX][MQ], int lane, float (&q)[F2MAX][MQ]) {
+#pragma unroll
+    for (int o = 0; o < F2MAX; ++o) {
+        if (o < F2) {
+            const int oz = o >= 2 ? opaque0_after(q[o >= 2 ? o - 2 : 0][0]) : opaque0();   // one row of lookahead
+            conv16_same<MQ>(d[o], prm + (g.o_w2 + o * K2 + oz), q[o], lane);
+        } else {
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) q[o][m] = 0.f;
+        }
+    }
+}
+
+// xh[j] = BN3-normalised r[j] = sum_i W3[j][i] q[i] (model.py:62-71; batch statistics of finalize 2)
+template <int MQ>
+__device__ __forceinline__ void pw_bn3(const Geo& g, const float* __restrict__ prm, const float* coef, int F2,
+                                       const float (&q)[F2MAX][MQ], float (&xh)[F2MAX][MQ]) {
+#pragma unroll
+    for (int j = 0; j < F2MAX; ++j) {
+        if (j < F2) {
+            const int oz = j >= 2 ? opaque0_after(xh[j >= 2 ? j - 2 : 0][0]) : opaque0();
+            const float* w3 = prm + (g.o_W3 + j * F2 + oz);
+            const float mu3 = coef[CF_MU3 * CSTR + j + oz], inv3 = coef[CF_INV3 * CSTR + j + oz];
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) {
+                float r = 0.f;
+#pragma unroll
+                for (int i = 0; i < F2MAX; ++i)
+                    if (i < F2) r = fmaf(w3[i], q[i][m], r);
+                xh[j][m] = (r - mu3) * inv3;
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) xh[j][m] = 0.f;
+        }
+    }
+}
+
+// ================================================================================================
+// Pass C: head (model.py:71-84).  logits, and (PC_BWD) CE, classifier grads, BN3-backward sums.
 // part row: [dWfc 4*NF][dbfc 4][Sdz3 F2][Sdz3x F2][loss]
+// Per-wave LDS: Hs [NF] -- the flattened head features (model.py:75 Flatten order), then their
+// gradients.
 // ================================================================================================
 template <int K1, int CC, int TT, int FF>
-__global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__ prm,
+__global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* __restrict__ prm,
                                                 const float* coef,    // the finalize writes it: no __restrict__
                                                 const float* __restrict__ d2g,
                                                 const uint8_t* __restrict__ mask3,
@@ -365,325 +517,397 @@ __global__ __launch_bounds__(NTH) void k_pass_c(Geo g, const float* __restrict__
                                                 float* __restrict__ part, int mode, FinArgs fa) {
     EEG_DIMS(g);
     TRACE(g, 2, TR_ENTRY);
+    constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
+    constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
+    const int NFP = rup4(NF);
+    const int nw = blockDim.x >> 6;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* D2s = sm;
-    float* Qs = D2s + F2 * RS2;
-    float* Hs = Qs + F2 * RS2;
-    float* DP3s = Hs + ((NF + 3) & ~3);
-    float* Ls = DP3s + ((NF + 3) & ~3);        // 8
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int o = wave;
-    const bool row_on = o < F2;
-    const int oo = row_on ? o : 0;
+    float* Hs = sm + wave * NFP;
 
-    for (int i = tid; i < 2 * F2 * RS2; i += NTH) sm[i] = 0.f;
-    float w2[K2], w3[F2MAX];
+    float wf[NCLS][NFQ], wacc[NCLS][NFQ];
 #pragma unroll
-    for (int k = 0; k < K2; ++k) w2[k] = prm[g.o_w2 + oo * K2 + k];
+    for (int n = 0; n < NCLS; ++n)
 #pragma unroll
-    for (int i = 0; i < F2MAX; ++i) w3[i] = i < F2 ? prm[g.o_W3 + oo * F2 + i] : 0.f;
-    const float mu3 = coef[CF_MU3 * CSTR + oo], inv3 = coef[CF_INV3 * CSTR + oo];
-    const float g3 = prm[g.o_g3 + oo], b3 = prm[g.o_b3 + oo];
-    // classifier-weight gradient items owned by this thread: p = tid + NTH * i < 4 * NF
-    constexpr int MAXW = 4;                      // NF <= 1024
-    float wacc[MAXW];
+        for (int u = 0; u < NFQ; ++u) {
+            const int i = lane + 64 * u;
+            wf[n][u] = i < NF ? prm[g.o_Wfc + n * NF + i] : 0.f;
+            wacc[n][u] = 0.f;
+        }
+    float sdz[2 * F2MAX];                 // [Sdz3 F2MAX][Sdz3x F2MAX], per-lane partials
 #pragma unroll
-    for (int i = 0; i < MAXW; ++i) wacc[i] = 0.f;
-    float bacc = 0.f, sdz = 0.f, sdzx = 0.f, lossacc = 0.f;
-    const int nd2 = F2 * T1;
-    float pfd[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int i = tid + NTH * j;
-        pfd[j] = ((int)blockIdx.x < g.B && i < nd2) ? d2g[(size_t)blockIdx.x * nd2 + i] : 0.f;
-    }
-    __syncthreads();
+    for (int j = 0; j < 2 * F2MAX; ++j) sdz[j] = 0.f;
+    float bacc[NCLS] = {0.f, 0.f, 0.f, 0.f}, lossacc = 0.f;
+    const float invB = 1.0f / (float)g.B;
 
     TRACE(g, 2, TR_PRO);
-    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+    TRACE_DECL();
+    drain_prologue_loads();
+    for (int b = blockIdx.x * nw + wave; b < g.B; b += gridDim.x * nw) {
+        float xh[F2MAX][MQ];
+        {
+            float d[F2MAX][MQ], q[F2MAX][MQ];
+            load_rows<MQ>(d2g, b, F2, T1, lane, d);
+            TRACE_PH(g, 2, 0, tph_);
+            dwconv_rows<MQ>(g, prm, F2, d, lane, q);
+            TRACE_PH(g, 2, 1, tph_);
+            pw_bn3<MQ>(g, prm, coef, F2, q, xh);
+        }
+        // ELU -> AvgPool(1,8) -> Hs (flattened index j*T2 + t/8)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = tid + NTH * j;
-            if (i < nd2) {
-                const int oo2 = i / T1, t = i - oo2 * T1;
-                D2s[oo2 * RS2 + LP2 + t] = pfd[j];
+        for (int j = 0; j < F2MAX; ++j) {
+            if (j >= F2) break;
+            const int oz = opaque0();
+            const float g3 = prm[g.o_g3 + j + oz], b3 = prm[g.o_b3 + j + oz];     // 2 scalars: fine hoisted
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) {
+                const int t = lane + 64 * m;
+                float e = t < 8 * T2 ? elu_f(fmaf(g3, xh[j][m], b3)) : 0.f;
+                e = sum8_hi(e);
+                if ((lane & 7) == 7 && t < 8 * T2) Hs[j * T2 + (t >> 3)] = e * 0.125f;
             }
         }
-        const int bn = b + gridDim.x;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = tid + NTH * j;
-            if (bn < g.B && i < nd2) pfd[j] = d2g[(size_t)bn * nd2 + i];
-        }
-        TRACE_PH(g, 2, 0, tph_);
-        __syncthreads();
-        float r[MAXT1Q];
-        block2_rows(F2, T1, RS2, D2s, Qs, w2, w3, row_on, o, lane, r);
-        TRACE_PH(g, 2, 1, tph_);
-        // BN3 (batch stats) -> ELU -> AvgPool(1,8) via 8-lane sums -> dropout -> h
-        float xh[MAXT1Q], z[MAXT1Q];
-#pragma unroll
-        for (int m = 0; m < MAXT1Q; ++m) {
-            const int t = lane + 64 * m;
-            xh[m] = (r[m] - mu3) * inv3;
-            z[m] = fmaf(g3, xh[m], b3);
-            float e = (row_on && t < 8 * T2) ? elu_f(z[m]) : 0.f;
-            e += __shfl_xor(e, 1, 64);
-            e += __shfl_xor(e, 2, 64);
-            e += __shfl_xor(e, 4, 64);
-            if (row_on && (t & 7) == 0 && t < 8 * T2) {
-                const int i = o * T2 + (t >> 3);
-                Hs[i] = e * 0.125f * keep_mul(g, mask3, 1, (size_t)b * NF + i);
-            }
-        }
-        __syncthreads();
+        wave_lds_fence();
         TRACE_PH(g, 2, 2, tph_);
-        if (wave < NCLS) {                        // logits (model.py:78-82): wave n -> class n
-            const int n = wave;
-            float a = 0.f;
-            for (int i = lane; i < NF; i += 64) a = fmaf(prm[g.o_Wfc + n * NF + i], Hs[i], a);
-            a = wave_sum(a);
-            if (lane == 0) Ls[n] = a + prm[g.o_bfc + n];
+        float hv[NFQ], kp[NFQ];
+#pragma unroll
+        for (int u = 0; u < NFQ; ++u) {
+            const int i = lane + 64 * u;
+            kp[u] = i < NF ? keep_mul(g, mask3, 1, (unsigned)(b * NF + i)) : 0.f;
+            hv[u] = i < NF ? Hs[i] * kp[u] : 0.f;          // dropout (model.py:74)
         }
-        __syncthreads();
-        TRACE_PH(g, 2, 3, tph_);
-        if ((mode & PC_LOGITS) && tid < NCLS) logits[(size_t)b * NCLS + tid] = Ls[tid];
+        // logits (model.py:78-82)
+        float lg[NCLS];
+#pragma unroll
+        for (int n = 0; n < NCLS; ++n) {
+            float a = 0.f;
+#pragma unroll
+            for (int u = 0; u < NFQ; ++u) a = fmaf(wf[n][u], hv[u], a);
+            lg[n] = a;
+        }
+        wave_reduce<NCLS>(lg);                              // lane 16n: class n
+        float L[NCLS];
+#pragma unroll
+        for (int n = 0; n < NCLS; ++n) L[n] = readlane_f(lg[0], 16 * n) + prm[g.o_bfc + n];
+        if ((mode & PC_LOGITS) && lane < NCLS)
+            logits[(size_t)b * NCLS + lane] = lane == 0 ? L[0] : lane == 1 ? L[1] : lane == 2 ? L[2] : L[3];
         if (mode & PC_BWD) {
-            if (tid == 0) {
-                float dl[NCLS];
-                if (mode & PC_CE) {                  // nn.CrossEntropyLoss, mean (train.py:103)
-                    float mx = Ls[0];
-                    for (int n = 1; n < NCLS; ++n) mx = fmaxf(mx, Ls[n]);
-                    float se = 0.f;
-                    for (int n = 0; n < NCLS; ++n) se += expf(Ls[n] - mx);
-                    const float lse = mx + logf(se);
-                    const int y = (int)labels[b];
-                    lossacc += lse - Ls[y];
-                    const float invB = 1.0f / (float)g.B;
-                    for (int n = 0; n < NCLS; ++n)
-                        dl[n] = (expf(Ls[n] - lse) - (n == y ? 1.f : 0.f)) * invB;
-                    for (int n = 0; n < NCLS; ++n) dlout[(size_t)b * NCLS + n] = dl[n];
-                } else {
-                    for (int n = 0; n < NCLS; ++n) dl[n] = dlin[(size_t)b * NCLS + n];
-                }
-                for (int n = 0; n < NCLS; ++n) Ls[4 + n] = dl[n];
-            }
-            __syncthreads();
-            TRACE_PH(g, 2, 4, tph_);
-            const float* DL = Ls + 4;
+            float dl[NCLS];
+            if (mode & PC_CE) {                              // nn.CrossEntropyLoss, mean (train.py:103)
+                const float mx = fmaxf(fmaxf(L[0], L[1]), fmaxf(L[2], L[3]));
+                float se = 0.f;
 #pragma unroll
-            for (int i = 0; i < MAXW; ++i) {
-                const int p = tid + NTH * i;
-                if (p < NCLS * NF) wacc[i] = fmaf(DL[p / NF], Hs[p % NF], wacc[i]);
-            }
-            if (tid < NCLS) bacc += DL[tid];
-            for (int i = tid; i < NF; i += NTH) {
-                float dh = 0.f;
+                for (int n = 0; n < NCLS; ++n) se += expf(L[n] - mx);
+                const float lse = mx + logf(se);
+                const int y = (int)labels[b];
+                const float Ly = y == 0 ? L[0] : y == 1 ? L[1] : y == 2 ? L[2] : L[3];
+                lossacc += lse - Ly;
 #pragma unroll
-                for (int n = 0; n < NCLS; ++n) dh = fmaf(DL[n], prm[g.o_Wfc + n * NF + i], dh);
-                DP3s[i] = dh * keep_mul(g, mask3, 1, (size_t)b * NF + i);
-            }
-            __syncthreads();
-            TRACE_PH(g, 2, 5, tph_);
-            if (row_on) {
+                for (int n = 0; n < NCLS; ++n) dl[n] = (expf(L[n] - lse) - (n == y ? 1.f : 0.f)) * invB;
+                if (lane < NCLS)
+                    dlout[(size_t)b * NCLS + lane] = lane == 0 ? dl[0] : lane == 1 ? dl[1] : lane == 2 ? dl[2] : dl[3];
+            } else {
 #pragma unroll
-                for (int m = 0; m < MAXT1Q; ++m) {
+                for (int n = 0; n < NCLS; ++n) dl[n] = dlin[(size_t)b * NCLS + n];
+            }
+#pragma unroll
+            for (int n = 0; n < NCLS; ++n) {
+                bacc[n] += dl[n];
+#pragma unroll
+                for (int u = 0; u < NFQ; ++u) wacc[n][u] = fmaf(dl[n], hv[u], wacc[n][u]);
+            }
+            // dh -> dropout -> dp3 (flattened), overwriting h in Hs (each lane its own slots)
+#pragma unroll
+            for (int u = 0; u < NFQ; ++u) {
+                const int i = lane + 64 * u;
+                float d = 0.f;
+#pragma unroll
+                for (int n = 0; n < NCLS; ++n) d = fmaf(dl[n], wf[n][u], d);
+                if (i < NF) Hs[i] = d * kp[u];
+            }
+            wave_lds_fence();
+            TRACE_PH(g, 2, 3, tph_);
+            // BN3-backward sums: dz3 = dp3/8 * ELU'(z3)
+#pragma unroll
+            for (int j = 0; j < F2MAX; ++j) {
+                if (j >= F2) break;
+                const int oz = opaque0();
+                const float g3 = prm[g.o_g3 + j + oz], b3 = prm[g.o_b3 + j + oz];
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) {
                     const int t = lane + 64 * m;
                     if (t < 8 * T2) {
-                        const float dz = DP3s[o * T2 + (t >> 3)] * 0.125f * elu_d(z[m]);
-                        sdz += dz;
-                        sdzx = fmaf(dz, xh[m], sdzx);
+                        const float dz = Hs[j * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3, xh[j][m], b3));
+                        sdz[j] += dz;
+                        sdz[F2MAX + j] = fmaf(dz, xh[j][m], sdz[F2MAX + j]);
                     }
                 }
             }
         }
-        __syncthreads();
-        TRACE_PH(g, 2, 6, tph_);
+        wave_lds_fence();
+        TRACE_PH(g, 2, 4, tph_);
     }
     TRACE_LOOP(g, 2);
-    if (mode & PC_BWD) {
-        float* row = part + (size_t)blockIdx.x * g.nC;
+    if (!(mode & PC_BWD)) return;
+    // ---- workgroup reduction: every wave writes a full partial row, then the waves are summed ----
+    __syncthreads();
+    float* red = sm;                         // [nw][nC]
+    float* rw = red + wave * g.nC;
 #pragma unroll
-        for (int i = 0; i < MAXW; ++i) {
-            const int p = tid + NTH * i;
-            if (p < NCLS * NF) pub(row + (p), wacc[i]);
+    for (int n = 0; n < NCLS; ++n)
+#pragma unroll
+        for (int u = 0; u < NFQ; ++u) {
+            const int i = lane + 64 * u;
+            if (i < NF) rw[n * NF + i] = wacc[n][u];
         }
-        if (tid < NCLS) pub(row + (NCLS * NF + tid), bacc);
-        const float a = wave_sum(sdz), ax = wave_sum(sdzx);
-        if (row_on && lane == 0) {
-            pub(row + (NCLS * NF + NCLS + o), a);
-            pub(row + (NCLS * NF + NCLS + F2 + o), ax);
+    wave_reduce<2 * F2MAX>(sdz);
+    if ((lane & 15) == 0) {
+        const int r0 = (lane >> 4) * (F2MAX / 2);
+#pragma unroll
+        for (int j = 0; j < F2MAX / 2; ++j) {
+            const int idx = j + r0;
+            if (idx < F2MAX) { if (idx < F2) rw[NCLS * NF + NCLS + idx] = sdz[j]; }
+            else if (idx - F2MAX < F2) rw[NCLS * NF + NCLS + F2 + idx - F2MAX] = sdz[j];
         }
-        if (tid == 0) pub(row + (NCLS * NF + NCLS + 2 * F2), lossacc);
-        double* dsm = (double*)sm;
-        if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
     }
+    if (lane == 0) {
+#pragma unroll
+        for (int n = 0; n < NCLS; ++n) rw[NCLS * NF + n] = bacc[n];
+        rw[NCLS * NF + NCLS + 2 * F2] = lossacc;
+    }
+    __syncthreads();
+    float* row = part + (size_t)blockIdx.x * g.nC;
+    for (int c = tid; c < g.nC; c += blockDim.x) {
+        float a = 0.f;
+        for (int w = 0; w < nw; ++w) a += red[w * g.nC + c];
+        pub(row + c, a);
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
 }
 
 // ================================================================================================
 // Pass D: block_2 backward (dW3, dw2), dp2 = d(pooled ELU output), BN2-backward sums.
 // part row: [dW3 F2*F2][dw2 F2*16][Sdz2 F2][Sdz2x F2]
+// Per-wave LDS rows (stride RSW): P0 d2 (pad LPD) | P1 q, then dq (pad LPQ) | P2 dr (pad LPQ) | Hs [NF].
 // ================================================================================================
 template <int K1, int CC, int TT, int FF>
-__global__ __launch_bounds__(NTH) void k_pass_d(Geo g, const float* __restrict__ prm,
-                                                const float* coef,    // the finalize writes it: no __restrict__
-                                                const float* __restrict__ d2g,
-                                                const float* __restrict__ E1g,
-                                                const float* __restrict__ E2g,
-                                                const uint8_t* __restrict__ mask2,
-                                                const uint8_t* __restrict__ mask3,
-                                                const float* __restrict__ dl,
-                                                float* __restrict__ dp2g, float* __restrict__ part,
-                                                FinArgs fa) {
+__global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict__ prm,
+                                                 const float* coef,    // the finalize writes it: no __restrict__
+                                                 const float* __restrict__ d2g,
+                                                 const float* __restrict__ E1g,
+                                                 const float* __restrict__ E2g,
+                                                 const uint8_t* __restrict__ mask2,
+                                                 const uint8_t* __restrict__ mask3,
+                                                 const float* __restrict__ dl,
+                                                 float* __restrict__ dp2g, float* __restrict__ part,
+                                                 FinArgs fa) {
     EEG_DIMS(g);
     TRACE(g, 3, TR_ENTRY);
+    constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
+    constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
+    const int RSW = TT ? row_stride_b2(TT / 4) : g.RSW;
+    const int NFP = rup4(NF);
+    const int nw = blockDim.x >> 6;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* D2s = sm;
-    float* Qs = D2s + F2 * RS2;        // q
-    float* DRs = Qs + F2 * RS2;        // dr
-    float* DQs = DRs + F2 * RS2;       // dq, padded LP2 | 8
-    float* DP3s = DQs + F2 * RS2;
     const int tid = threadIdx.x, lane = tid & 63;
+    const int li = lane & 15, lk = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int o = wave;
-    const bool row_on = o < F2;
-    const int oo = row_on ? o : 0;
+    float* P0 = sm + wave * (3 * F2 * RSW + NFP);
+    float* P1 = P0 + F2 * RSW;
+    float* P2 = P1 + F2 * RSW;
+    float* Hs = P2 + F2 * RSW;
 
-    for (int i = tid; i < 4 * F2 * RS2; i += NTH) sm[i] = 0.f;
-    float w2[K2], w3[F2MAX], w3c[F2MAX];
+    for (int i = lane; i < 3 * F2 * RSW; i += 64) P0[i] = 0.f;   // pads stay zero
+    float wf[NCLS][NFQ];
 #pragma unroll
-    for (int k = 0; k < K2; ++k) w2[k] = prm[g.o_w2 + oo * K2 + k];
+    for (int n = 0; n < NCLS; ++n)
 #pragma unroll
-    for (int i = 0; i < F2MAX; ++i) {
-        w3[i] = i < F2 ? prm[g.o_W3 + oo * F2 + i] : 0.f;     // row o of W3 (pw forward)
-        w3c[i] = i < F2 ? prm[g.o_W3 + i * F2 + oo] : 0.f;    // column o of W3 (dq)
-    }
-    const float mu3 = coef[CF_MU3 * CSTR + oo], inv3 = coef[CF_INV3 * CSTR + oo];
-    const float g3 = prm[g.o_g3 + oo], b3 = prm[g.o_b3 + oo];
-    const float A3 = coef[CF_A3 * CSTR + oo], B3 = coef[CF_B3 * CSTR + oo], C3 = coef[CF_C3 * CSTR + oo];
-    float dW3p[F2MAX], dw2p[K2];
+        for (int u = 0; u < NFQ; ++u) {
+            const int i = lane + 64 * u;
+            wf[n][u] = i < NF ? prm[g.o_Wfc + n * NF + i] : 0.f;
+        }
+    floatx4 acc3 = {0.f, 0.f, 0.f, 0.f};        // dW3 tile: D[j = 4 lk + r][i = li]
+    const int o2 = lane >> 2, kq = lane & 3;   // dw2 item of this lane: row o2, taps 4 kq .. 4 kq + 3
+    float acc2[4] = {0.f, 0.f, 0.f, 0.f};
+    float sz[2 * F2MAX];                       // [Sdz2 F2MAX][Sdz2x F2MAX], per-lane partials
 #pragma unroll
-    for (int i = 0; i < F2MAX; ++i) dW3p[i] = 0.f;
-#pragma unroll
-    for (int k = 0; k < K2; ++k) dw2p[k] = 0.f;
-    float sz = 0.f, szx = 0.f;
-    const int nd2 = F2 * T1;
-    float pfd[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int i = tid + NTH * j;
-        pfd[j] = ((int)blockIdx.x < g.B && i < nd2) ? d2g[(size_t)blockIdx.x * nd2 + i] : 0.f;
-    }
-    __syncthreads();
+    for (int j = 0; j < 2 * F2MAX; ++j) sz[j] = 0.f;
+    const int nkg = (T1 + 15) >> 4, ntq = (T1 + 3) >> 2;
+    wave_lds_fence();
 
     TRACE(g, 3, TR_PRO);
-    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+    TRACE_DECL();
+    drain_prologue_loads();
+    for (int b = blockIdx.x * nw + wave; b < g.B; b += gridDim.x * nw) {
+        float dlv[NCLS];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = tid + NTH * j;
-            if (i < nd2) {
-                const int oo2 = i / T1, t = i - oo2 * T1;
-                D2s[oo2 * RS2 + LP2 + t] = pfd[j];
-            }
-        }
-        const int bn = b + gridDim.x;
+        for (int n = 0; n < NCLS; ++n) dlv[n] = dl[(size_t)b * NCLS + n];
+        float d[F2MAX][MQ];
+        load_rows<MQ>(d2g, b, F2, T1, lane, d);
+        // d2 rows -> P0 (read back by the dw2 correlation)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = tid + NTH * j;
-            if (bn < g.B && i < nd2) pfd[j] = d2g[(size_t)bn * nd2 + i];
-        }
-        // dh -> dp3 (independent of block_2): DP3s[i] = (dl . Wfc[:,i]) * keep
-        for (int i = tid; i < NF; i += NTH) {
-            float dh = 0.f;
+        for (int o = 0; o < F2MAX; ++o)
 #pragma unroll
-            for (int n = 0; n < NCLS; ++n) dh = fmaf(dl[(size_t)b * NCLS + n], prm[g.o_Wfc + n * NF + i], dh);
-            DP3s[i] = dh * keep_mul(g, mask3, 1, (size_t)b * NF + i);
-        }
-        __syncthreads();
-        float r[MAXT1Q];
-        block2_rows(F2, T1, RS2, D2s, Qs, w2, w3, row_on, o, lane, r);
-        // BN3 backward with the batch constants of finalize 3: dr = A3 dz3 + B3 + C3 xh3
-        if (row_on) {
-#pragma unroll
-            for (int m = 0; m < MAXT1Q; ++m) {
+            for (int m = 0; m < MQ; ++m) {
                 const int t = lane + 64 * m;
-                if (t < T1) {
-                    const float xh = (r[m] - mu3) * inv3;
-                    const float z = fmaf(g3, xh, b3);
-                    const float dz = (t < 8 * T2) ? DP3s[o * T2 + (t >> 3)] * 0.125f * elu_d(z) : 0.f;
-                    const float d = fmaf(A3, dz, fmaf(C3, xh, B3));
-                    DRs[o * RS2 + t] = d;
-                    // dW3[o][i] += dr[o][t] q[i][t]
+                if (o < F2 && t < T1) P0[o * RSW + LPD + t] = d[o][m];
+            }
+        // dh -> dropout -> dp3 (flattened) into Hs
 #pragma unroll
-                    for (int i = 0; i < F2MAX; ++i)
-                        if (i < F2) dW3p[i] = fmaf(d, Qs[i * RS2 + t], dW3p[i]);
+        for (int u = 0; u < NFQ; ++u) {
+            const int i = lane + 64 * u;
+            float dd = 0.f;
+#pragma unroll
+            for (int n = 0; n < NCLS; ++n) dd = fmaf(dlv[n], wf[n][u], dd);
+            if (i < NF) Hs[i] = dd * keep_mul(g, mask3, 1, (unsigned)(b * NF + i));
+        }
+        float q[F2MAX][MQ];
+        dwconv_rows<MQ>(g, prm, F2, d, lane, q);
+#pragma unroll
+        for (int o = 0; o < F2MAX; ++o)
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) {
+                const int t = lane + 64 * m;
+                if (o < F2 && t < T1) P1[o * RSW + LPQ + t] = q[o][m];
+            }
+        wave_lds_fence();
+        // BN3 backward with the batch constants of finalize 3: dr = A3 dz3 + B3 + C3 xh3,
+        // dz3 = dp3/8 * ELU'(z3); zero beyond T1 (the dq / dd2 shifts read it)
+        float dr[F2MAX][MQ];
+        {
+            float xh[F2MAX][MQ];
+            pw_bn3<MQ>(g, prm, coef, F2, q, xh);
+#pragma unroll
+            for (int j = 0; j < F2MAX; ++j) {
+                if (j < F2) {
+                    const int oz = opaque0();
+                    const float g3 = prm[g.o_g3 + j + oz], b3 = prm[g.o_b3 + j + oz];
+                    const float A3 = coef[CF_A3 * CSTR + j + oz], B3 = coef[CF_B3 * CSTR + j + oz];
+                    const float C3 = coef[CF_C3 * CSTR + j + oz];
+#pragma unroll
+                    for (int m = 0; m < MQ; ++m) {
+                        const int t = lane + 64 * m;
+                        const float dz = t < 8 * T2 ? Hs[j * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3, xh[j][m], b3)) : 0.f;
+                        dr[j][m] = t < T1 ? fmaf(A3, dz, fmaf(C3, xh[j][m], B3)) : 0.f;
+                        if (t < T1) P2[j * RSW + LPQ + t] = dr[j][m];
+                    }
+                } else {
+#pragma unroll
+                    for (int m = 0; m < MQ; ++m) dr[j][m] = 0.f;
                 }
             }
         }
-        __syncthreads();
-        if (row_on) {
-            // dq[o][t] = sum_j W3[j][o] dr[j][t]
+        wave_lds_fence();
+        // E1 / E2 of pass B for the BN2-backward sums at the end (issued here, consumed last)
+        float e1v[F2MAX][MQ], e2v[F2MAX][MQ];
+        load_rows<MQ>(E1g, b, F2, T1, lane, e1v);
+        load_rows<MQ>(E2g, b, F2, T1, lane, e2v);
+        // dW3[j][i] += sum_t dr[j][t] q[i][t] on the matrix cores (float4 k-permuted operands)
+        {
+            const bool on = li < F2;
+            const float* ar = P2 + (on ? li : 0) * RSW + LPQ + 4 * lk;
+            const float* br = P1 + (on ? li : 0) * RSW + LPQ + 4 * lk;
+            for (int kg = 0; kg < nkg; ++kg) {
+                floatx4 a4 = lds_ld4(ar + 16 * kg), b4 = lds_ld4(br + 16 * kg);
+                if (!on) { a4 = (floatx4){0.f, 0.f, 0.f, 0.f}; b4 = a4; }
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], acc3, 0, 0, 0);
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], acc3, 0, 0, 0);
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], acc3, 0, 0, 0);
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], acc3, 0, 0, 0);
+            }
+        }
+        wave_lds_fence();                          // q rows consumed before dq overwrites them
+        // dq[i][t] = sum_j W3[j][i] dr[j][t] (registers, and P1 for the dw2 correlation)
+        float dq[F2MAX][MQ];
 #pragma unroll
-            for (int m = 0; m < MAXT1Q; ++m) {
-                const int t = lane + 64 * m;
-                if (t < T1) {
+        for (int i = 0; i < F2MAX; ++i) {
+            if (i < F2) {
+                const int oz = i >= 2 ? opaque0_after(dq[i >= 2 ? i - 2 : 0][0]) : opaque0();
+                const float* w3c = prm + (g.o_W3 + i + oz);      // column i of W3 (stride F2)
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) {
+                    const int t = lane + 64 * m;
                     float a = 0.f;
 #pragma unroll
                     for (int j = 0; j < F2MAX; ++j)
-                        if (j < F2) a = fmaf(w3c[j], DRs[j * RS2 + t], a);
-                    DQs[o * RS2 + LP2 + t] = a;
+                        if (j < F2) a = fmaf(w3c[j * F2], dr[j][m], a);
+                    dq[i][m] = a;
+                    if (t < T1) P1[i * RSW + LPQ + t] = a;
                 }
-            }
-            wave_lds_fence();
-            const float* dqr = DQs + o * RS2 + LP2;
-            const float* d2r = D2s + o * RS2 + 1;
+            } else {
 #pragma unroll
-            for (int m = 0; m < MAXT1Q; ++m) {
+                for (int m = 0; m < MQ; ++m) dq[i][m] = 0.f;
+            }
+        }
+        wave_lds_fence();
+        // dw2[o][k] += sum_t dq[o][t] d2p[o][t+k-7]: lane -> (row o2, taps 4 kq + kk), loop over t
+        if (o2 < F2) {
+            const float* dqr = P1 + o2 * RSW + LPQ;
+            const float* d2r = P0 + o2 * RSW + 4 * kq;      // d2p[t + k - 7] = P0[row + t + k]
+            for (int tq = 0; tq < ntq; ++tq) {
+                const floatx4 a4 = lds_ld4(dqr + 4 * tq);
+                const floatx4 w0 = lds_ld4(d2r + 4 * tq), w1 = lds_ld4(d2r + 4 * tq + 4);
+                const float w[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc2[kk] = fmaf(a4[i], w[i + kk], acc2[kk]);
+            }
+        }
+        // dd2 = conv16_same_t(dq) -> dropout -> dp2; BN2-backward sums (E1/E2 of pass B)
+        const size_t rb = (size_t)b * F2 * T1;
+#pragma unroll
+        for (int o = 0; o < F2MAX; ++o) {
+            if (o >= F2) break;
+            float a[MQ];
+            const int oz = o >= 2 ? opaque0_after(sz[o >= 2 ? o - 2 : 0]) : opaque0();
+            conv16_same_t<MQ>(dq[o], prm + (g.o_w2 + o * K2 + oz), a, lane);
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) {
                 const int t = lane + 64 * m;
                 if (t < T1) {
-                    const float dq = dqr[t];
-                    // dw2[o][k] += dq[o][t] d2pad[o][t+k]
-#pragma unroll
-                    for (int k = 0; k < K2; ++k) dw2p[k] = fmaf(dq, d2r[t + k], dw2p[k]);
-                    // dd2[o][t] = sum_k w2[o][k] dq[o][t+7-k]
-                    float a = 0.f;
-#pragma unroll
-                    for (int k = 0; k < K2; ++k) a = fmaf(w2[k], dqr[t + 7 - k], a);
-                    const size_t gi = ((size_t)b * F2 + o) * T1 + t;
-                    const float dp = a * keep_mul(g, mask2, 0, gi);
-                    dp2g[gi] = dp;
-                    sz = fmaf(dp * 0.25f, E1g[gi], sz);
-                    szx = fmaf(dp * 0.25f, E2g[gi], szx);
+                    const int gi = o * T1 + t;
+                    const float dp = a[m] * keep_mul(g, mask2, 0, (unsigned)(rb + gi));
+                    dp2g[rb + gi] = dp;
+                    sz[o] = fmaf(dp * 0.25f, e1v[o][m], sz[o]);
+                    sz[F2MAX + o] = fmaf(dp * 0.25f, e2v[o][m], sz[F2MAX + o]);
                 }
             }
         }
-        __syncthreads();
+        wave_lds_fence();
     }
     TRACE_LOOP(g, 3);
-    float* row = part + (size_t)blockIdx.x * g.nD;
-    {
-        constexpr int NR = F2MAX + K2 + 4, NQ = NR / 4;   // [dW3 F2MAX][dw2 K2][sz][szx][pad 2]
-        float rv[NR];
+    // ---- workgroup reduction ----
+    __syncthreads();
+    float* red = sm;                         // [nw][nD]
+    float* rw = red + wave * g.nD;
 #pragma unroll
-        for (int i = 0; i < F2MAX; ++i) rv[i] = dW3p[i];
+    for (int r = 0; r < 4; ++r) {
+        const int j = 4 * lk + r;
+        if (j < F2 && li < F2) rw[j * F2 + li] = acc3[r];
+    }
+    if (o2 < F2) {
 #pragma unroll
-        for (int k = 0; k < K2; ++k) rv[F2MAX + k] = dw2p[k];
-        rv[F2MAX + K2] = sz; rv[F2MAX + K2 + 1] = szx; rv[F2MAX + K2 + 2] = 0.f; rv[F2MAX + K2 + 3] = 0.f;
-        wave_reduce<NR>(rv);
-        if (row_on && (lane & 15) == 0) {
-            const int r0 = (lane >> 4) * NQ;
+        for (int kk = 0; kk < 4; ++kk) rw[F2 * F2 + o2 * K2 + 4 * kq + kk] = acc2[kk];
+    }
+    wave_reduce<2 * F2MAX>(sz);
+    if ((lane & 15) == 0) {
+        const int r0 = (lane >> 4) * (F2MAX / 2);
 #pragma unroll
-            for (int j = 0; j < NQ; ++j) {
-                const int idx = j + r0;
-                if (idx < F2MAX) { if (idx < F2) pub(row + (o * F2 + idx), rv[j]); }
-                else if (idx < F2MAX + K2) pub(row + (F2 * F2 + o * K2 + idx - F2MAX), rv[j]);
-                else if (idx == F2MAX + K2) pub(row + (F2 * F2 + 16 * F2 + o), rv[j]);
-                else if (idx == F2MAX + K2 + 1) pub(row + (F2 * F2 + 17 * F2 + o), rv[j]);
-            }
+        for (int j = 0; j < F2MAX / 2; ++j) {
+            const int idx = j + r0;
+            if (idx < F2MAX) { if (idx < F2) rw[F2 * F2 + 16 * F2 + idx] = sz[j]; }
+            else if (idx - F2MAX < F2) rw[F2 * F2 + 17 * F2 + idx - F2MAX] = sz[j];
         }
+    }
+    __syncthreads();
+    float* row = part + (size_t)blockIdx.x * g.nD;
+    for (int c = tid; c < g.nD; c += blockDim.x) {
+        float a = 0.f;
+        for (int w = 0; w < nw; ++w) a += red[w * g.nD + c];
+        pub(row + c, a);
     }
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
@@ -731,9 +955,12 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
     const float al = coef[CF_AL2 * CSTR + oo], be = coef[CF_BE2 * CSTR + oo];
     const float ga = prm[g.o_g2 + oo], bt = prm[g.o_b2 + oo];
     const float Ao = coef[CF_AO * CSTR + oo], Bo = coef[CF_BO * CSTR + oo], Co = coef[CF_CO * CSTR + oo];
-    float Q[K1];
+    // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] of this wave's row on the matrix
+    // cores (lagcorr_mfma); the tiles stay in registers for the whole workgroup
+    constexpr int NTQ = (K1 + 16) / 16;
+    floatx4 qacc[NTQ];
 #pragma unroll
-    for (int k = 0; k < K1; ++k) Q[k] = 0.f;
+    for (int i = 0; i < NTQ; ++i) qacc[i] = (floatx4){0.f, 0.f, 0.f, 0.f};
     float sdy = 0.f, sdyv = 0.f;
     // dws GEMM split: wave -> (c-tile ct, k-group range)
     const int wpc = NWAVE / NCT;
@@ -757,7 +984,8 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
 
     int it = 0;
     TRACE(g, 4, TR_PRO);
-    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
+    TRACE_DECL();
+    drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = (it & 1) ? Xb1 : Xb0;
         float* Xn = (it & 1) ? Xb0 : Xb1;
@@ -770,7 +998,10 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
                 if (i < ndp) pdp[j] = dp2g[(size_t)bn * ndp + i];
             }
         }
+        #ifndef EXP_NO_SPAT
         spatial_mfma<KS>(Xc, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+#endif
+
         TRACE_PH(g, 4, 0, tph_);
         __syncthreads();                                   // Ss, DP complete
         TRACE_PH(g, 4, 1, tph_);
@@ -795,18 +1026,14 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
                     sdy += d;
                     sdyv = fmaf(d, v[i], sdyv);
                 }
-                // dW1 correlation: Q[k] += sum_i dy[i] * spad[t0+i+k]
-#pragma unroll
-                for (int k = 0; k < K1; ++k) {
-                    float a = Q[k];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) a = fmaf(dy[i], w[G_::OFF + i + k], a);
-                    Q[k] = a;
-                }
                 lds_st4(drow + 4 * q, (floatx4){dy[0], dy[1], dy[2], dy[3]});
             }
             TRACE_PH(g, 4, 2, tph_);
             wave_lds_fence();
+#ifndef EXP_NO_LAG
+            lagcorr_mfma<NTQ>(Dys + o * RS + LP, Ss + o * RS + LP, T, NT16, g.P, qacc, lane);
+#endif
+            wave_lds_fence();                              // s row consumed before e overwrites it
             // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
             const float* dyr = Dys + o * RS;
             float* erow = Ss + o * RS + LP;
@@ -831,7 +1058,11 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
         TRACE_PH(g, 4, 5, tph_);
         // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
         // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
+#ifdef EXP_NO_DWS
+        if (false) {
+#else
         if (gemm_on) {
+#endif
             const int c = ct * 16 + li;
             const float* arow = Ss + (li < F2 ? li : 0) * RS + LP + 4 * lk;
             const float* brow = Xc + (c < C ? c : 0) * RS + LP + 4 * lk;
@@ -868,23 +1099,17 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
     // ---- reductions ----
     float* row = part + (size_t)blockIdx.x * g.nE;
     {
-        constexpr int NR = K1 + 4, NQ = NR / 4;         // [Q K1][sdy][sdyv][pad 2]
-        float rv[NR];
-#pragma unroll
-        for (int k = 0; k < K1; ++k) rv[k] = Q[k];
-        rv[K1] = sdy; rv[K1 + 1] = sdyv; rv[K1 + 2] = 0.f; rv[K1 + 3] = 0.f;
-        wave_reduce<NR>(rv);
-        if (row_on && (lane & 15) == 0) {
-            const int r0 = (lane >> 4) * NQ;
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) {
-                const int idx = j + r0;
-                if (idx < K1) pub(row + (o * K1 + idx), rv[j]);
-                else if (idx == K1) pub(row + (F2 * K1 + F2 * C + o), rv[j]);
-                else if (idx == K1 + 1) pub(row + (F2 * K1 + F2 * C + F2 + o), rv[j]);
-            }
-        }
+        float rv[4] = {sdy, sdyv, 0.f, 0.f};
+        wave_reduce<4>(rv);                              // lane 0: sum dy, lane 16: sum dy v
+        if (row_on && (lane == 0 || lane == 16))
+            pub(row + (F2 * K1 + F2 * C + (lane ? F2 : 0) + o), rv[0]);
     }
+    // Q[o][k] = sum_i M_o[i][i+k] from this wave's lag-correlation tiles (LDS after the Xm slab)
+    float* Ms = red + NWAVE * 256;                   // [NWAVE][16][16 NTQ]
+#pragma unroll
+    for (int nt = 0; nt < NTQ; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ms[(wave * 16 + 4 * lk + r) * (16 * NTQ) + 16 * nt + li] = qacc[nt][r];
     // Xm: wave -> 16x16 tile partial (rows 4lk+r, col li) -> LDS [wave][256] -> sum over the
     // waves of each c-tile
 #pragma unroll
@@ -896,6 +1121,14 @@ __global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Ad
         float a = 0.f;
         for (int w = ct2 * wpc; w < (ct2 + 1) * wpc; ++w) a += red[w * 256 + oo2 * 16 + cc];
         pub(row + (F2 * K1 + p), a);
+    }
+    for (int p = tid; p < F2 * K1; p += NTH) {
+        const int oo2 = p / K1, k = p - oo2 * K1;
+        const float* Mo = Ms + oo2 * 16 * (16 * NTQ);
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a += Mo[i * (16 * NTQ) + i + k];
+        pub(row + p, a);
     }
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nE, fa, dsm)) { fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa); TRACE(g, 4, TR_FIN); }
@@ -959,7 +1192,8 @@ __global__ __launch_bounds__(NTH) void k_infer(Geo g, const float* __restrict__ 
 
     int it = 0;
     TRACE(g, 5, TR_PRO);
-    unsigned long long tph_ = clock64(), tacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; (void)tph_; (void)tacc_;
+    TRACE_DECL();
+    drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
         const float* Xc = Xb0;
         float* Xn = Xb0;

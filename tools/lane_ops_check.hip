@@ -12,15 +12,18 @@ __global__ void k(float* out) {
     out[128 + l] = __builtin_bit_cast(float, q[0]);
     out[192 + l] = __builtin_bit_cast(float, q[1]);
     out[256 + l] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x124, 0xF, 0xF, false));
+    out[320 + l] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x138, 0xF, 0xF, true));  // wave_shr:1
+    out[384 + l] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x130, 0xF, 0xF, true));  // wave_shl:1
+    out[448 + l] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), 0x114, 0xF, 0xF, true));  // row_shr:4
 }
 int main() {
-    float* d; hipMalloc(&d, 320 * 4);
+    float* d; hipMalloc(&d, 512 * 4);
     k<<<1, 64>>>(d);
-    float h[320]; hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-    const char* nm[5] = {"p32.x", "p32.y", "p16.x", "p16.y", "ror4"};
-    for (int r = 0; r < 5; ++r) {
+    float h[512]; hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    const char* nm[8] = {"p32.x", "p32.y", "p16.x", "p16.y", "ror4", "wshr1", "wshl1", "rshr4"};
+    for (int r = 0; r < 8; ++r) {
         printf("%s:", nm[r]);
-        for (int l = 0; l < 64; l += 4) printf(" %g", h[r * 64 + l]);
+        for (int l = 0; l < 64; l += (r >= 5 ? 1 : 4)) printf(" %g", h[r * 64 + l]);
         printf("\n");
     }
     return 0;
