@@ -32,7 +32,7 @@ _SIGS = {
     "eegnet_param_count": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(ctypes.c_int64)]),
     "eegnet_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(ctypes.c_size_t)]),
     "eegnet_forward_train": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp,
-                                            ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp]),
+                                            ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp]),
     "eegnet_backward": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp, _vp,
                                        ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp, _vp,
                                        ctypes.c_int]),
@@ -43,7 +43,7 @@ _SIGS = {
     "eegnet_train_step": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, ctypes.c_uint64,
                                          ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
-                                         _vp, _vp, ctypes.c_int]),
+                                         _vp, _vp, ctypes.c_int, _vp]),
     "eegnet_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "eegnet_profile_collect": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp, ctypes.c_int, _vp]),
     "eegnet_trace_enable": (ctypes.c_int, [_vp]),

@@ -46,7 +46,6 @@ struct Geo {
     int nH, nTl, nedge;  // lag-Gram edge terms: head pairs R(R+1)/2, tail pairs P(P+1)/2, + R + P sums
     float p, scale, eps, mom;
     int drop;
-    int xdb;             // pass E: double-buffered x rows
     int noclamp;         // skip the model.py:44/84 clamps (data-parallel: clamp after all-reduce)
     unsigned long long key;
     unsigned key0, key1;  // per-layer 32-bit dropout keys (derived from key)
@@ -55,8 +54,8 @@ struct Geo {
     int o_w1, o_g1, o_b1, o_ws, o_g2, o_b2, o_w2, o_W3, o_g3, o_b3, o_Wfc, o_bfc, nparam;
     // partial-row lengths of the five passes and the (common) workgroup count
     int nA, nB, nC, nD, nE;
-    int grid;
-    int rgs, ngrp;       // in-kernel reduction: partial rows per group, groups (<= NGRPMAX)
+    int grid;            // workgroups of passes C, D and the eval forward
+    int gridS;           // workgroups of the streaming passes A, B, E (two per CU)
     // LDS (floats)
     int ldsA, ldsB, ldsC, ldsD, ldsE, ldsI;
     // optional timeline instrumentation (eegnet_trace_enable): [pass][workgroup][TR_SLOTS] stamps
@@ -119,6 +118,7 @@ enum PassCMode { PC_LOGITS = 1, PC_BWD = 2, PC_CE = 4 };
 // pass's finalize.  Ticket words: NCNT per pass, zeroed by a memset node at the start of every call.
 constexpr int NGRPMAX = 15;
 constexpr int NCNT = 16;          // [0, ngrp) group tickets, [NCNT-1] the top-level ticket
+constexpr int TK_PASSES = 5;      // ticket blocks: passes A..E, contiguous from pass A's
 struct FinArgs {
     double* part2;                // [ngrp][ncols] fp64 group partials
     unsigned* cnt;                // this pass's NCNT ticket words
@@ -127,6 +127,7 @@ struct FinArgs {
     float* bn;                    // running statistics (fin1/fin2, when update_running)
     float* grads;
     float* loss;
+    int64_t* nbt;                 // BatchNorm num_batches_tracked x3 (fin2 increments; nullable)
     int update_running, ce;
     int tpass;                    // pass index for the timeline stamps
     // Adam (torch.optim.Adam) fused into pass E's finalize when adam_m != nullptr
@@ -144,9 +145,10 @@ __host__ __device__ constexpr int row_stride(int K1, int T) {
     // rows of x / s / dy / e: [LP zeros | T samples | >= R zeros]; long enough for the last 4-output
     // FIR window and the last 16-column MFMA tile; RS/4 odd so that column reads of 16 rows (MFMA
     // operands) land in 16 different bank groups
-    const int P = (K1 - 1) / 2, R = K1 - 1 - P, LP = (R + 3) & ~3, OFF = LP - P;
+    const int P = (K1 - 1) / 2, R = K1 - 1 - P, LP = (R + 3) & ~3, OFF = LP - P, OFFD = LP - R;
     const int NW = (OFF + K1 + 6) / 4, TQ = (T + 3) / 4, NT16 = (T + 15) / 16;
-    const int rs = rup4(imax(imax(4 * (TQ - 1) + 4 * NW, LP + 16 * NT16), LP + T + R));
+    const int NW8 = (imax(OFF, OFFD) + K1 + 10) / 4, NO = (T + 7) / 8;     // 8-output windows
+    const int rs = rup4(imax(imax(imax(4 * (TQ - 1) + 4 * NW, 8 * (NO - 1) + 4 * NW8), LP + 16 * NT16), LP + T + R));
     return ((rs / 4) & 1) ? rs : rs + 4;
 }
 __host__ __device__ constexpr int row_stride2(int T) { return rup4(LP2 + T / 4 + 8); }
@@ -166,14 +168,21 @@ struct KG {
     static constexpr int OFF = LP - P;              // window offset of the forward FIR / Gram
     static constexpr int OFFD = LP - R;             // window offset of the transposed FIR
     static constexpr int NW = (OFF + K1 + 3 + 3) / 4;   // float4s per 4-output window
-    static constexpr int NEI = ((R * (R + 1) / 2 + P * (P + 1) / 2 + R + P) + NTH - 1) / NTH;
+    static constexpr int NW8 = ((OFF > OFFD ? OFF : OFFD) + K1 + 7 + 3) / 4;   // float4s per 8-output window
+    // lag-Gram edge items per thread of an NT-thread workgroup
+    template <int NT>
+    static constexpr int nei() { return ((R * (R + 1) / 2 + P * (P + 1) / 2 + R + P) + NT - 1) / NT; }
 };
 
 // ------------------------------------------------------------------------------------------------
 // device helpers
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : expm1f(z); }
-__device__ __forceinline__ float elu_d(float z) { return z > 0.f ? 1.f : expf(z); }
+// ELU (alpha = 1) and its derivative on the hardware exp2 (v_exp_f32): exp(z) = 2^(z log2 e), a
+// few ulp for the |z| BatchNorm produces -- against ~12 instructions for libm's expf / expm1f.
+// Below 0 the absolute error of exp(z) - 1 is that of exp(z) (~1e-7), far inside the parity bar.
+__device__ __forceinline__ float fast_exp(float z) { return __builtin_amdgcn_exp2f(z * 1.4426950408889634f); }
+__device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : fast_exp(z) - 1.f; }
+__device__ __forceinline__ float elu_d(float z) { return z > 0.f ? 1.f : fast_exp(z); }
 
 // Dropout keep factor (model.py:50,74 nn.Dropout: x * mask / (1-p)).  Injected masks win; otherwise a
 // counter-based draw: murmur3's 32-bit finalizer of (flat index * golden ratio + per-layer key), top
@@ -237,6 +246,21 @@ __device__ __forceinline__ float row_sum16(float v) {
     return v;
 }
 
+// N independent sums over each half-wave (lanes 0-31, 32-63) at once (N % 2 == 0): one halving
+// swap then 4 DPP steps on N/2 registers.  On return v[j] holds, in lane 0 / 16 / 32 / 48, the sum of
+// value j / j + N/2 over half-wave 0 / 0 / 1 / 1 (every lane of a 16-lane row holds the same).
+template <int N>
+__device__ __forceinline__ void half_reduce(float (&v)[N]) {
+    static_assert(N % 2 == 0, "half_reduce: N must be even");
+#pragma unroll
+    for (int j = 0; j < N / 2; ++j) {
+        swap16(v[j], v[j + N / 2]);
+        v[j] += v[j + N / 2];
+    }
+#pragma unroll
+    for (int j = 0; j < N / 2; ++j) v[j] = row_sum16(v[j]);
+}
+
 // sum over the 64 lanes, result in every lane
 __device__ __forceinline__ float wave_sum(float v) {
     float a = v, b = v;
@@ -296,16 +320,28 @@ __device__ __forceinline__ void fir4(const float (&w)[NWF], const float (&tap)[K
     }
 }
 
+// 8 outputs of a K-tap correlation from a window: out[i] = sum_k tap[k] * w[OFF + i + k]; two
+// independent 4-output chains per lane -- twice the FMAs per LDS window of fir4
+template <int K, int OFF, int NWF>
+__device__ __forceinline__ void fir8(const float (&w)[NWF], const float (&tap)[K], float (&out)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[i] = fmaf(tap[k], w[OFF + i + k], out[i]);
+}
+
 // ---- x staging: global -> registers (issued a whole trial ahead) -> LDS rows ----
 // PF floats per thread cover one trial: C*T <= NTH*PF.
-template <int PF>
+template <int PF, int NT = NTH>
 __device__ __forceinline__ void x_prefetch(const float* __restrict__ xb, int C, int T, float (&pf)[PF], int tid) {
     const int n = C * T;
     if ((T & 3) == 0) {
         const float4* src = reinterpret_cast<const float4*>(xb);
 #pragma unroll
         for (int j = 0; j < PF / 4; ++j) {
-            const int i = tid + NTH * j;
+            const int i = tid + NT * j;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (4 * i < n) v = src[i];
             pf[4 * j] = v.x; pf[4 * j + 1] = v.y; pf[4 * j + 2] = v.z; pf[4 * j + 3] = v.w;
@@ -313,20 +349,20 @@ __device__ __forceinline__ void x_prefetch(const float* __restrict__ xb, int C, 
     } else {
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
-            const int i = tid + NTH * j;
+            const int i = tid + NT * j;
             pf[j] = i < n ? xb[i] : 0.f;
         }
     }
 }
 
-template <int PF>
+template <int PF, int NT = NTH>
 __device__ __forceinline__ void x_store(const float (&pf)[PF], int C, int T, int RS, int LP, float* Xs, int tid) {
     const int n = C * T;
     if ((T & 3) == 0) {
         const int TQ = T >> 2;
 #pragma unroll
         for (int j = 0; j < PF / 4; ++j) {
-            const int i = tid + NTH * j;
+            const int i = tid + NT * j;
             if (4 * i < n) {
                 const int c = i / TQ, q = i - c * TQ;
                 lds_st4(Xs + c * RS + LP + 4 * q, (floatx4){pf[4 * j], pf[4 * j + 1], pf[4 * j + 2], pf[4 * j + 3]});
@@ -335,7 +371,7 @@ __device__ __forceinline__ void x_store(const float (&pf)[PF], int C, int T, int
     } else {
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
-            const int i = tid + NTH * j;
+            const int i = tid + NT * j;
             if (i < n) {
                 const int c = i / T, t = i - c * T;
                 Xs[c * RS + LP + t] = pf[j];
@@ -360,12 +396,12 @@ __device__ __forceinline__ void load_ws_frag(const float* __restrict__ ws, int C
 // s[o,t] = sum_c ws[o,c] x[c,t] on the matrix cores: v_mfma_f32_16x16x4_f32, A = ws (registers),
 // B = x tile (4 c x 16 t).  Lane l: A[l&15][l>>4], B[l>>4][l&15]; D[4(l>>4)+r][l&15] (CDNA4 maps).
 // Exact f32 (a k-ordered fmaf chain).  Wave w computes column tiles w, w+16, ...
-template <int KS>
+template <int KS, int NW = NWAVE>
 __device__ __forceinline__ void spatial_mfma(const float* Xs, const float (&aw)[KS], float* Ss, int C, int F2,
                                              int NT16, int RS, int LP, int wave, int lane) {
     const int li = lane & 15, lk = lane >> 4;
     const int ks = (C + 3) >> 2;
-    for (int n = wave; n < NT16; n += NWAVE) {
+    for (int n = wave; n < NT16; n += NW) {
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
         const float* xcol = Xs + lk * RS + LP + 16 * n + li;
 #pragma unroll
@@ -406,8 +442,11 @@ __device__ __forceinline__ void lagcorr_mfma(const float* a, const float* b, int
     }
 }
 
-// Static shape of a kernel instantiation: CC/TT/FF = 0 means "runtime value from Geo".
-#define EEG_DIMS(g)                                                                         \
+// Static shape of a kernel instantiation: CC/TT/FF = 0 means "runtime value from Geo".  The
+// specialised shapes are EEGNet-8,2 (F2 = 16, D = 2); PF = x prefetch floats per thread of an
+// NT_-thread workgroup.
+#define EEG_DIMS(g) EEG_DIMS_NT(g, NTH)
+#define EEG_DIMS_NT(g, NT_)                                                                 \
     const int C = CC ? CC : (g).C;                                                          \
     const int T = TT ? TT : (g).T;                                                          \
     const int F2 = FF ? FF : (g).F2;                                                        \
@@ -416,7 +455,7 @@ __device__ __forceinline__ void lagcorr_mfma(const float* a, const float* b, int
     const int RS2 = TT ? row_stride2(TT) : (g).RS2;                                         \
     const int NT16 = (T + 15) >> 4, NCT = (C + 15) >> 4;                                    \
     constexpr int LP = KG<K1>::LP;                                                          \
-    constexpr int PF = (CC && TT) ? ((CC * TT + NTH - 1) / NTH + 3) / 4 * 4 : 16;            \
+    constexpr int PF = (CC && TT) ? ((CC * TT + (NT_) - 1) / (NT_) + 3) / 4 * 4 : MAXPF * NTH / (NT_); \
     constexpr int KS = CC ? (CC + 3) / 4 : 16;                                              \
     (void)TQ; (void)T1; (void)T2; (void)NF; (void)RS2; (void)NT16; (void)NCT; (void)LP
 

@@ -9,8 +9,8 @@ namespace eeg {
 // In-kernel deterministic fp64 reduction of the per-workgroup partial rows (cdna_hip_programming.md
 // §6 Guideline 16, counter form).  Every workgroup of a pass publishes its row (write-through stores,
 // every wave drains, barrier, one lane: relaxed agent ticket add).  The last arriver of
-// each group of g.rgs rows sums the group's rows in fp64 (agent acquire first) into part2; the last
-// of those group reducers sums the g.ngrp group partials into S (LDS) and runs the pass's finalize.
+// each group of rgs rows sums the group's rows in fp64 (agent acquire first) into part2; the last
+// of those group reducers sums the ngrp group partials into S (LDS) and runs the pass's finalize.
 // The summation order is fixed by (row, column) alone, so results do not depend on arrival order.
 // ================================================================================================
 
@@ -53,8 +53,11 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     int* flag = (int*)dsm;
     double* S = dsm + 2;
     double* scr = dsm + tail_s_doubles(ncols);
-    const int grp = blockIdx.x / g.rgs;
-    const int r0 = grp * g.rgs, r1 = min(g.grid, r0 + g.rgs), nr = r1 - r0;
+    // partial rows per group / groups from this launch's own grid (passes use different grids)
+    const int grid = gridDim.x;
+    const int rgs = max(32, (grid + NGRPMAX - 1) / NGRPMAX), ngrp = (grid + rgs - 1) / rgs;
+    const int grp = blockIdx.x / rgs;
+    const int r0 = grp * rgs, r1 = min(grid, r0 + rgs), nr = r1 - r0;
     const int tp = fa.tpass;
     TRACE(g, tp, TR_PUB);
     if (!take_ticket(fa.cnt + grp, (unsigned)nr, flag)) return false;
@@ -82,18 +85,18 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
         pub(fa.part2 + (size_t)grp * ncols + c, a);
     }
     TRACE(g, tp, TR_GRP);
-    if (!take_ticket(fa.cnt + (NCNT - 1), (unsigned)g.ngrp, flag)) return false;
+    if (!take_ticket(fa.cnt + (NCNT - 1), (unsigned)ngrp, flag)) return false;
     for (int c = tid; c < ncols; c += (int)blockDim.x) {
         double v[NGRPMAX];
 #pragma unroll
-        for (int q = 0; q < NGRPMAX; ++q) v[q] = q < g.ngrp ? fa.part2[(size_t)q * ncols + c] : 0.0;
+        for (int q = 0; q < NGRPMAX; ++q) v[q] = q < ngrp ? fa.part2[(size_t)q * ncols + c] : 0.0;
         double a = 0.0;
 #pragma unroll
-        for (int q = 0; q < NGRPMAX; ++q) if (q < g.ngrp) a += v[q];
+        for (int q = 0; q < NGRPMAX; ++q) if (q < ngrp) a += v[q];
         S[c] = a;
     }
     // every ticket of this pass has been taken: re-arm them (the per-call memset is the guarantee)
-    if (tid < g.ngrp) __hip_atomic_store(fa.cnt + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < ngrp) __hip_atomic_store(fa.cnt + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) __hip_atomic_store(fa.cnt + (NCNT - 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     TRACE(g, tp, TR_TOP);
@@ -220,6 +223,8 @@ __device__ void fin2(const Geo& g, const double* sums, const FinArgs& fa) {
     fa.coef[CF_INV3 * CSTR + j] = (float)(1.0 / sqrt(var + (double)g.eps));
     float* rm3 = fa.bn + 2 * g.F1 + 2 * g.F2;
     if (fa.update_running) bn_running(rm3 + j, rm3 + g.F2 + j, mu, var, n3, g.mom);
+    // BatchNorm2d.num_batches_tracked += 1 for the three BN layers (train-mode forward)
+    if (fa.update_running && fa.nbt && j < 3) fa.nbt[j] += 1;
 }
 
 // after pass C: classifier grads (+ clamp, model.py:84), BN3 grads and backward constants

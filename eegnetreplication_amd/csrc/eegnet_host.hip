@@ -41,16 +41,6 @@ static int device_cus() {
     return cus;
 }
 
-// workgroups resident per CU for the streaming passes (EEGNET_WGPC, default 1; experiment knob)
-static int wg_per_cu() {
-    static int v = 0;
-    if (v == 0) {
-        const char* e = getenv("EEGNET_WGPC");
-        v = e ? std::max(1, std::min(2, atoi(e))) : 1;
-    }
-    return v;
-}
-
 static unsigned long long* g_trace_buf = nullptr;     // eegnet_trace_enable
 
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
@@ -70,15 +60,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->T1 = g->T / 4; g->T2 = g->T1 / 8; g->NF = g->F2 * g->T2;
     g->LP = (g->R + 3) & ~3;
     g->TQ = (g->T + 3) / 4; g->NT16 = (g->T + 15) / 16; g->NKG = g->NT16;
-    {
-        const int OFF = g->LP - g->P;
-        const int NW = (OFF + g->K1 + 6) / 4;
-        int rs = std::max(4 * (g->TQ - 1) + 4 * NW, g->LP + 16 * g->NT16);
-        rs = std::max(rs, g->LP + g->T + g->R);
-        rs = rup(rs, 4);
-        if (((rs / 4) & 1) == 0) rs += 4;      // RS/4 odd: column reads of 16 rows hit 16 banks
-        g->RS = rs;
-    }
+    g->RS = row_stride(g->K1, g->T);
     g->RS2 = rup(LP2 + g->T1 + 8, 4);
     g->CK = rup(g->C, 4); g->NCT = (g->C + 15) / 16;
     g->nH = g->R * (g->R + 1) / 2;
@@ -107,25 +89,22 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nC = NCLS * g->NF + NCLS + 2 * g->F2 + 1;
     g->nD = g->F2 * g->F2 + 18 * g->F2;
     g->nE = g->F2 * g->K1 + g->F2 * g->C + 2 * g->F2;
-    g->grid = std::min(g->B, device_cus() * wg_per_cu());
-    g->rgs = std::max(32, (g->grid + NGRPMAX - 1) / NGRPMAX);
-    g->ngrp = (g->grid + g->rgs - 1) / g->rgs;
-    const int rows1 = g->C * g->RS;                   // x rows (A, B, infer: one buffer)
-    const int rows2 = 2 * g->C * g->RS;               // double-buffered x rows (E)
+    g->grid = std::min(g->B, device_cus());             // passes C, D, infer
+    g->gridS = std::min(g->B, device_cus() * WGPC);     // streaming passes A, B, E
+    const int rows1 = g->C * g->RS;                   // x rows (one buffer)
     const int nf4 = rup(g->NF, 4);
-    g->ldsA = rows1 + g->F2 * g->RS + NWAVE * (g->K1 + 1);
-    g->ldsB = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2;
+    g->ldsA = rows1 + g->F2 * g->RS + NWB * (g->K1 + 1);
+    g->ldsB = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + F2MAX * (K2 + F2MAX);
     // passes C / D: one trial stream per wave, each with its own block-2 rows (row_stride_b2)
     g->RSW = row_stride_b2(g->T1);
     const int pwC = nf4, pwD = 3 * g->F2 * g->RSW + nf4;
-    const bool spec = g->C == 22 && (g->T == 256 || g->T == 257) && g->F2 == 16 && g->K1 == 32;   // EEG_DISPATCH
+    const bool spec = g->C == 22 && (g->T == 256 || g->T == 257) && g->F1 == 8 && g->D == 2 && g->K1 == 32;   // EEG_DISPATCH
     g->nwC = std::max(1, std::min(spec ? NWAVE : NTHS / 64, (LDS_MAX / 4) / pwC));
     g->nwD = std::max(1, std::min(NTHS / 64, (LDS_MAX / 4) / pwD));
     g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);
     g->ldsD = std::max(g->nwD * pwD, g->nwD * g->nD);
-    g->ldsE = 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4);
-    g->xdb = (wg_per_cu() == 1 && (g->ldsE + rows2) * 4 <= LDS_MAX) ? 1 : 0;
-    g->ldsE = std::max(g->ldsE + (g->xdb ? rows2 : rows1), NWAVE * 256 + NWAVE * 16 * (g->K1 + 16));   // + lag tiles
+    g->ldsE = std::max(rows1 + 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4),
+                       NWB * 256);                                // after the loop: dws tiles
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
     auto tail = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + std::max(tail_scratch_doubles(ncols), fin)); };
@@ -158,11 +137,11 @@ static WsLayout make_layout(const Geo& g) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = rupz(o + bytes, 256); return r; };
     L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
-    L.partA = take((size_t)g.grid * g.nA * 4);
-    L.partB = take((size_t)g.grid * g.nB * 4);
+    L.partA = take((size_t)g.gridS * g.nA * 4);
+    L.partB = take((size_t)g.gridS * g.nB * 4);
     L.partC = take((size_t)g.grid * g.nC * 4);
     L.partD = take((size_t)g.grid * g.nD * 4);
-    L.partE = take((size_t)g.grid * g.nE * 4);
+    L.partE = take((size_t)g.gridS * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
     L.sums = take((size_t)nmax * 8 * NGRPMAX);
     L.stats = take((size_t)(g.K1 * g.K1 + g.K1) * 8);
@@ -246,14 +225,14 @@ static void ensure_attrs() {
 // runs the runtime-shape instantiation of the same kernels
 #define EEG_DISPATCH(K1_, g_, LAUNCH)                                                            \
     do {                                                                                         \
-        if ((K1_) == 32 && (g_).C == 22 && (g_).T == 256 && (g_).F2 == 16) { LAUNCH(32, 22, 256, 16); } \
-        else if ((K1_) == 32 && (g_).C == 22 && (g_).T == 257 && (g_).F2 == 16) { LAUNCH(32, 22, 257, 16); } \
+        if ((K1_) == 32 && (g_).C == 22 && (g_).T == 256 && (g_).F1 == 8 && (g_).D == 2) { LAUNCH(32, 22, 256, 16); } \
+        else if ((K1_) == 32 && (g_).C == 22 && (g_).T == 257 && (g_).F1 == 8 && (g_).D == 2) { LAUNCH(32, 22, 257, 16); } \
         else { LAUNCH(K1_, 0, 0, 0); }                                                           \
     } while (0)
 
 // the finalize arguments of one pass (ticket words `tk`); Adam is attached to pass E by the caller
 static FinArgs fin_args(const WsLayout& L, char* ws, int tk, float* bn, float* grads, float* loss,
-                        int update_running, int ce) {
+                        int update_running, int ce, int64_t* nbt = nullptr) {
     FinArgs f;
     memset(&f, 0, sizeof(f));
     f.part2 = (double*)(ws + L.sums);
@@ -262,28 +241,22 @@ static FinArgs fin_args(const WsLayout& L, char* ws, int tk, float* bn, float* g
     f.coef = (float*)(ws + L.coef);
     f.bn = bn; f.grads = grads; f.loss = loss;
     f.update_running = update_running; f.ce = ce;
+    f.nbt = nbt;
     f.tpass = tk;
     return f;
 }
 
-// zero the ticket words (cdna_hip_programming.md §6 Guideline 16: re-initialise every call)
-static int reset_tickets(const WsLayout& L, char* ws, hipStream_t s) {
-    PROF(KID_MEMSET);
-    if (hipMemsetAsync(ws + L.cnt, 0, CNT_BYTES, s) != hipSuccess)
-        return fail(EEGNET_ELAUNCH, "hipMemsetAsync(tickets): %s", hipGetErrorString(hipGetLastError()));
-    return 0;
-}
 
 template <int K1>
 static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
-                       const float* x, const uint8_t* m2, int update_running, hipStream_t s) {
+                       const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s) {
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
-    const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0);
-#define LAUNCH_A(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsA * 4, s, \
+    const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
+#define LAUNCH_A(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridS), dim3(NTB), g.ldsA * 4, s, \
                                                    g, params, x, (float*)(ws + L.partA), fa)
     { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
     } LAUNCH_CHECK("k_pass_a");
-#define LAUNCH_B(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsB * 4, s, \
+#define LAUNCH_B(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.gridS), dim3(NTB), g.ldsB * 4, s, \
                        g, params, (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), \
                        (float*)(ws + L.E2), (float*)(ws + L.partB), fb)
     { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
@@ -317,7 +290,7 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        (float*)(ws + L.partD), fd)
     { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
     } LAUNCH_CHECK("k_pass_d");
-#define LAUNCH_E(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsE * 4, s, \
+#define LAUNCH_E(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridS), dim3(NTB), g.ldsE * 4, s, \
                        g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe)
     { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
     } LAUNCH_CHECK("k_pass_e");
@@ -350,7 +323,8 @@ int eegnet_workspace_bytes(const eegnet_dims* dims, size_t* out) {
 
 int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn_buffers,
                          const float* x, const uint8_t* mask2, const uint8_t* mask3,
-                         uint64_t seed, uint64_t offset, float* logits, void* ws, void* stream) {
+                         uint64_t seed, uint64_t offset, float* logits, void* ws, void* stream,
+                         int64_t* num_batches_tracked) {
     Geo g;
     if (int r = make_geo(dims, &g)) return r;
     if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
@@ -362,9 +336,8 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
-    if (int r = reset_tickets(L, w, s)) return r;
-    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, mask2, 1, s)
-                       : run_forward<64>(g, L, w, params, bn_buffers, x, mask2, 1, s);
+    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, mask2, 1, num_batches_tracked, s)
+                       : run_forward<64>(g, L, w, params, bn_buffers, x, mask2, 1, num_batches_tracked, s);
     if (r) return r;
     FinArgs none;
     memset(&none, 0, sizeof(none));
@@ -393,7 +366,6 @@ int eegnet_backward(const eegnet_dims* dims, const float* params, const float* x
     const WsLayout L = make_layout(g);
     const int mode = PC_BWD | (dlogits ? 0 : PC_CE);
     hipStream_t s = (hipStream_t)stream;
-    if (int r = reset_tickets(L, (char*)ws, s)) return r;
     float* p = const_cast<float*>(params);        // written only by a fused Adam, which this call has not
     return g.K1 == 32
         ? run_backward<32>(g, L, (char*)ws, p, x, mask2, mask3, dlogits, labels, nullptr, grads, loss, mode, nullptr, s)
@@ -433,7 +405,8 @@ int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_av
 int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers, const float* x,
                       const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
                       float* adam_state, int32_t* step, float lr, float beta1, float beta2,
-                      float eps, float* loss, float* logits, void* ws, void* stream, int flags) {
+                      float eps, float* loss, float* logits, void* ws, void* stream, int flags,
+                      int64_t* num_batches_tracked) {
     Geo g;
     if (int r = make_geo(dims, &g)) return r;
     if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
@@ -447,9 +420,8 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
-    if (int r = reset_tickets(L, w, s)) return r;
-    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, 1, s)
-                       : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, 1, s);
+    int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s)
+                       : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s);
     if (r) return r;
     const int mode = PC_BWD | PC_CE | (logits ? PC_LOGITS : 0);
     // Adam runs in pass E's finalize; adam_state == NULL: gradients only (data-parallel: all-reduce,

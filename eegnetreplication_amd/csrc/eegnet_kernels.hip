@@ -36,5 +36,6 @@
 #include "../../include/eegnet_abi.h"
 #include "eegnet_common.h"
 #include "eegnet_finalize.hip"
+#include "eegnet_stream.hip"
 #include "eegnet_passes.hip"
 #include "eegnet_host.hip"

@@ -1,323 +1,12 @@
-// eegnet_passes.hip -- the five streaming passes of the restructured EEGNet train step and the
-// fused eval-mode forward.  Included by eegnet_kernels.hip (one translation unit).
+// eegnet_passes.hip -- the block-2-rate passes C and D of the restructured EEGNet train step and
+// the fused eval-mode forward.  Included by eegnet_kernels.hip (one translation unit); the passes
+// that stream x (A, B, E) are in eegnet_stream.hip.
 //
-// Workgroup = 1024 threads = 16 waves, one workgroup per CU, trials strided over the grid.  Wave w
-// owns output row o = w of every per-trial [F2, T] plane (F2 <= 16), so its FIR taps are
-// wave-uniform (SGPRs), the FIR windows it reads are lane-contiguous float4s (no LDS bank
-// conflicts), and its per-row partial sums live in registers until the workgroup ends.  The next
-// trial's x is fetched into registers a whole trial ahead and lands in the second LDS buffer.
+// k_infer: workgroup = 1024 threads = 16 waves, one workgroup per CU, trials strided over the
+// grid.  Wave w owns output row o = w of every per-trial [F2, T] plane (F2 <= 16), so its FIR taps
+// are wave-uniform (SGPRs) and the FIR windows it reads are lane-contiguous float4s.
 
 namespace eeg {
-
-// ================================================================================================
-// Pass A: BN1 / BN2 batch statistics (model.py:32, 47).
-// part row: [G0 K1][S0][H nH][Tl nTl][hs R][ts P][Sv F2][Sv2 F2]
-//   G0[d] = sum_{c,t<T} X[t] X[t+d]       (lag-Gram of the padded rows, window start 0)
-//   H[a,b] = sum_c x[a] x[b], 0<=a<=b<R    (head outer products -> Gram edge corrections)
-//   Tl[u,v] = sum_c x[T-P+u] x[T-P+v]     (tail outer products)
-//   hs / ts = head / tail sample sums       (window-sum corrections)
-//   Sv, Sv2 = sum v, sum v^2 per row o      (BN2: y2 = a1 v + c1 W)
-// ================================================================================================
-template <int K1, int CC, int TT, int FF>
-__global__ __launch_bounds__(NTH) void k_pass_a(Geo g, const float* __restrict__ prm,
-                                                const float* __restrict__ x, float* __restrict__ part,
-                                                FinArgs fa) {
-    using G_ = KG<K1>;
-    EEG_DIMS(g);
-    TRACE(g, 0, TR_ENTRY);
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* const Xb0 = sm;             // one x buffer: the next trial lands after its last reader
-    float* Ss = sm + C * RS;
-    float* red = Ss + F2 * RS;                        // NWAVE * (K1 + 1)
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-    for (int i = tid; i < (C + F2) * RS; i += NTH) sm[i] = 0.f;
-    float aw[KS];
-    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
-
-    // FIR row (wave-uniform) and its taps
-    const int o = wave;
-    const bool fir_on = o < F2;
-    float tap[K1];
-    {
-        const int gg = (fir_on ? o : 0) / g.D;
-#pragma unroll
-        for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + gg * K1 + k];
-    }
-    float sv = 0.f, sv2 = 0.f;
-    float G0[K1];
-#pragma unroll
-    for (int d = 0; d < K1; ++d) G0[d] = 0.f;
-    float s0 = 0.f;
-    // edge items: decode (row-index a, row-index b) once; b < 0 -> a plain sample sum
-    float eacc[G_::NEI];
-    int ea[G_::NEI], eb[G_::NEI];
-#pragma unroll
-    for (int i = 0; i < G_::NEI; ++i) {
-        eacc[i] = 0.f;
-        int e = tid + NTH * i;
-        ea[i] = -1; eb[i] = -1;
-        if (e < g.nH) {                                  // head pair (a <= b < R), a-major
-            int a = 0;
-            while (e >= g.R - a) { e -= g.R - a; ++a; }
-            ea[i] = a; eb[i] = a + e;
-        } else if ((e -= g.nH) < g.nTl) {                // tail pair (u <= v < P)
-            int u = 0;
-            while (e >= g.P - u) { e -= g.P - u; ++u; }
-            ea[i] = T - g.P + u; eb[i] = T - g.P + u + e;
-        } else if ((e -= g.nTl) < g.R) {
-            ea[i] = e;
-        } else if ((e -= g.R) < g.P) {
-            ea[i] = T - g.P + e;
-        } else {
-            ea[i] = -2;                                  // unused slot
-        }
-    }
-    float pf[PF];
-    if ((int)blockIdx.x < g.B) x_prefetch<PF>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
-    __syncthreads();
-    x_store<PF>(pf, C, T, RS, LP, Xb0, tid);
-    __syncthreads();
-
-    int it = 0;
-    TRACE(g, 0, TR_PRO);
-    TRACE_DECL();
-    drain_prologue_loads();
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
-        const float* Xc = Xb0;
-        float* Xn = Xb0;
-        const int bn = b + gridDim.x;
-        if (bn < g.B) x_prefetch<PF>(x + (size_t)bn * C * T, C, T, pf, tid);
-        spatial_mfma<KS>(Xc, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
-        // lag-Gram: items (c, quad), lanes of a wave on consecutive quads of one row
-        for (int j = tid; j < C * TQ; j += NTH) {
-            const int c = j / TQ, q = j - c * TQ;
-            float w[4 * G_::NW];
-            lds_window<G_::NW>(Xc + c * RS + 4 * q, w);
-            float a[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = (4 * q + i < T) ? w[G_::OFF + i] : 0.f;
-            s0 += (a[0] + a[1]) + (a[2] + a[3]);
-#pragma unroll
-            for (int d = 0; d < K1; ++d) {
-                float acc = G0[d];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc = fmaf(a[i], w[G_::OFF + i + d], acc);
-                G0[d] = acc;
-            }
-        }
-        // edge outer products / sums over channels
-#pragma unroll
-        for (int i = 0; i < G_::NEI; ++i) {
-            if (ea[i] >= 0) {
-                const float* xa = Xc + LP + ea[i];
-                float acc0 = 0.f, acc1 = 0.f;
-                if (eb[i] >= 0) {
-                    const float* xb2 = Xc + LP + eb[i];
-                    int c = 0;
-                    for (; c + 1 < C; c += 2) {
-                        acc0 = fmaf(xa[c * RS], xb2[c * RS], acc0);
-                        acc1 = fmaf(xa[(c + 1) * RS], xb2[(c + 1) * RS], acc1);
-                    }
-                    if (c < C) acc0 = fmaf(xa[c * RS], xb2[c * RS], acc0);
-                } else {
-                    int c = 0;
-                    for (; c + 1 < C; c += 2) { acc0 += xa[c * RS]; acc1 += xa[(c + 1) * RS]; }
-                    if (c < C) acc0 += xa[c * RS];
-                }
-                eacc[i] += acc0 + acc1;
-            }
-        }
-        TRACE_PH(g, 0, 0, tph_);
-        __syncthreads();                                   // Ss complete
-        TRACE_PH(g, 0, 1, tph_);
-        if (fir_on) {
-            const float* row = Ss + o * RS;
-            for (int q = lane; q < TQ; q += 64) {
-                float w[4 * G_::NW];
-                lds_window<G_::NW>(row + 4 * q, w);
-                float v[4];
-                fir4<K1, G_::OFF>(w, tap, v);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (4 * q + i < T) { sv += v[i]; sv2 = fmaf(v[i], v[i], sv2); }
-            }
-        }
-        TRACE_PH(g, 0, 2, tph_);
-        if (bn < g.B) x_store<PF>(pf, C, T, RS, LP, Xn, tid);
-        TRACE_PH(g, 0, 3, tph_);
-        __syncthreads();                                   // Xn staged, Ss free
-        TRACE_PH(g, 0, 4, tph_);
-    }
-    TRACE_LOOP(g, 0);
-
-    // ---- workgroup reduction -> one partial row ----
-    float* row = part + (size_t)blockIdx.x * g.nA;
-    {
-        constexpr int NR = K1 + 4, NQ = NR / 4;       // [G0 K1][s0][sv][sv2][pad]
-        float rv[NR];
-#pragma unroll
-        for (int d = 0; d < K1; ++d) rv[d] = G0[d];
-        rv[K1] = s0; rv[K1 + 1] = sv; rv[K1 + 2] = sv2; rv[K1 + 3] = 0.f;
-        wave_reduce<NR>(rv);
-        if ((lane & 15) == 0) {
-            const int r0 = (lane >> 4) * NQ;
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) {
-                const int idx = j + r0;
-                if (idx <= K1) red[wave * (K1 + 1) + idx] = rv[j];
-                else if (fir_on && idx == K1 + 1) pub(row + (K1 + 1 + g.nedge + o), rv[j]);
-                else if (fir_on && idx == K1 + 2) pub(row + (K1 + 1 + g.nedge + F2 + o), rv[j]);
-            }
-        }
-    }
-    __syncthreads();
-    if (tid <= K1) {
-        float t = 0.f;
-        for (int w = 0; w < NWAVE; ++w) t += red[w * (K1 + 1) + tid];
-        pub(row + (tid), t);
-    }
-#pragma unroll
-    for (int i = 0; i < G_::NEI; ++i)
-        if (ea[i] != -2 && tid + NTH * i < g.nedge) pub(row + (K1 + 1 + tid + NTH * i), eacc[i]);
-    double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nA, fa, dsm)) { fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa); TRACE(g, 0, TR_FIN); }
-}
-
-// ================================================================================================
-// Pass B: forward to d2, E1/E2 (pooled ELU' sums for the BN2 backward), BN3 statistics.
-// part row: [Sr F2][Sr2 F2]
-// ================================================================================================
-template <int K1, int CC, int TT, int FF>
-__global__ __launch_bounds__(NTH) void k_pass_b(Geo g, const float* __restrict__ prm,
-                                                const float* coef,    // the finalize writes it: no __restrict__
-                                                const float* __restrict__ x,
-                                                const uint8_t* __restrict__ mask2,
-                                                float* __restrict__ d2g, float* __restrict__ E1g,
-                                                float* __restrict__ E2g, float* __restrict__ part,
-                                                FinArgs fa) {
-    using G_ = KG<K1>;
-    EEG_DIMS(g);
-    TRACE(g, 1, TR_ENTRY);
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* const Xb0 = sm;             // one x buffer: the next trial lands after its last reader
-    float* Ss = sm + C * RS;
-    float* D2s = Ss + F2 * RS;
-    float* Qs = D2s + F2 * RS2;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-    for (int i = tid; i < (C + F2) * RS + 2 * F2 * RS2; i += NTH) sm[i] = 0.f;
-    float aw[KS];
-    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
-    const int o = wave;
-    const bool row_on = o < F2;
-    const int oo = row_on ? o : 0;
-    float tap[K1];
-    {
-        const int gg = oo / g.D;
-#pragma unroll
-        for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + gg * K1 + k];
-    }
-    float w2[K2], w3[F2MAX];
-#pragma unroll
-    for (int k = 0; k < K2; ++k) w2[k] = prm[g.o_w2 + oo * K2 + k];
-#pragma unroll
-    for (int i = 0; i < F2MAX; ++i) w3[i] = i < F2 ? prm[g.o_W3 + oo * F2 + i] : 0.f;
-    const float al = coef[CF_AL2 * CSTR + oo], be = coef[CF_BE2 * CSTR + oo];
-    const float ga = prm[g.o_g2 + oo], bt = prm[g.o_b2 + oo];
-    float sr = 0.f, sr2 = 0.f;
-    float pf[PF];
-    if ((int)blockIdx.x < g.B) x_prefetch<PF>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
-    __syncthreads();
-    x_store<PF>(pf, C, T, RS, LP, Xb0, tid);
-    __syncthreads();
-
-    int it = 0;
-    TRACE(g, 1, TR_PRO);
-    TRACE_DECL();
-    drain_prologue_loads();
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
-        const float* Xc = Xb0;
-        float* Xn = Xb0;
-        const int bn = b + gridDim.x;
-        if (bn < g.B) x_prefetch<PF>(x + (size_t)bn * C * T, C, T, pf, tid);
-        spatial_mfma<KS>(Xc, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
-        __syncthreads();                                   // Ss complete; Qs free
-        // d2 / E1 / E2 of this row stay in registers until the next trial's x is staged: a global
-        // store issued before that x_store would hold its vmcnt wait (loads and stores drain in order)
-        float d2v[MAXT1Q], e1v[MAXT1Q], e2v[MAXT1Q];
-        if (row_on) {
-            const float* row = Ss + o * RS;
-            float* drow = D2s + o * RS2 + LP2;
-#pragma unroll
-            for (int m = 0; m < MAXT1Q; ++m) {             // pool-4 windows = quads
-                const int q = lane + 64 * m;
-                if (q >= T1) break;
-                float w[4 * G_::NW];
-                lds_window<G_::NW>(row + 4 * q, w);
-                float v[4];
-                fir4<K1, G_::OFF>(w, tap, v);
-                float pe = 0.f, e1 = 0.f, e2 = 0.f;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float xh = fmaf(al, v[i], be);
-                    const float z = fmaf(ga, xh, bt);
-                    const float dz = elu_d(z);
-                    pe += z > 0.f ? z : dz - 1.f;          // ELU(z) = exp(z) - 1 below 0
-                    e1 += dz;
-                    e2 = fmaf(dz, xh, e2);
-                }
-                const size_t gi = ((size_t)b * F2 + o) * T1 + q;
-                const float d2 = pe * 0.25f * keep_mul(g, mask2, 0, gi);
-                d2v[m] = d2; e1v[m] = e1; e2v[m] = e2;
-                drow[q] = d2;
-            }
-            wave_lds_fence();
-            // depthwise 1x16 'same' conv of this row (model.py:54-61): pad 7 | 8
-            const float* dr = D2s + o * RS2 + 1;
-            for (int t = lane; t < T1; t += 64) {
-                float a = 0.f;
-#pragma unroll
-                for (int k = 0; k < K2; ++k) a = fmaf(w2[k], dr[t + k], a);
-                Qs[o * RS2 + t] = a;
-            }
-        }
-        if (bn < g.B) x_store<PF>(pf, C, T, RS, LP, Xn, tid);
-        if (row_on) {
-#pragma unroll
-            for (int m = 0; m < MAXT1Q; ++m) {
-                const int q = lane + 64 * m;
-                if (q >= T1) break;
-                const size_t gi = ((size_t)b * F2 + o) * T1 + q;
-                d2g[gi] = d2v[m]; E1g[gi] = e1v[m]; E2g[gi] = e2v[m];
-            }
-        }
-        __syncthreads();                                   // Qs complete, Xn staged
-        if (row_on) {                                      // pointwise F2 x F2 (model.py:62-69)
-            for (int t = lane; t < T1; t += 64) {
-                float r = 0.f;
-#pragma unroll
-                for (int i = 0; i < F2MAX; ++i)
-                    if (i < F2) r = fmaf(w3[i], Qs[i * RS2 + t], r);
-                sr += r;
-                sr2 = fmaf(r, r, sr2);
-            }
-        }
-    }
-    TRACE_LOOP(g, 1);
-    {
-        float rv[4] = {sr, sr2, 0.f, 0.f};
-        wave_reduce<4>(rv);                        // lane 0: sum sr, lane 16: sum sr2
-        if (row_on && (lane == 0 || lane == 16)) {
-            float* row = part + (size_t)blockIdx.x * g.nB;
-            pub(row + (lane ? F2 + o : o), rv[0]);
-        }
-    }
-    double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nB, fa, dsm)) { fin2(g, dsm + 2, fa); TRACE(g, 1, TR_FIN); }
-}
 
 // block_2 forward of one trial in the row-per-wave layout: D2s (padded d2 rows) -> q (Qs) -> r.
 // Returns r[m] for t = lane + 64 m (m < MAXT1Q) of row o.  Contains one workgroup barrier.
@@ -911,227 +600,6 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
     }
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
-}
-
-// ================================================================================================
-// Pass E: dy2 and the weight-gradient reductions that need full-rate data.
-// part row: [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2]
-// ================================================================================================
-template <int K1, int CC, int TT, int FF>
-__global__ __launch_bounds__(NTH) void k_pass_e(Geo g, const float* prm,   // Adam (finalize) writes it
-                                                const float* coef,    // the finalize writes it: no __restrict__
-                                                const float* __restrict__ x,
-                                                const float* __restrict__ dp2g,
-                                                float* __restrict__ part, FinArgs fa) {
-    using G_ = KG<K1>;
-    EEG_DIMS(g);
-    TRACE(g, 4, TR_ENTRY);
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    // x rows double-buffered when LDS allows (g.xdb): the next trial lands during phase B; otherwise
-    // one buffer refilled after the dws GEMM, behind one extra barrier
-    const bool xdb = g.xdb != 0;
-    float* const Xb0 = sm;
-    float* const Xb1 = sm + (xdb ? C * RS : 0);
-    float* Ss = sm + (xdb ? 2 : 1) * C * RS;     // s, then e
-    float* Dys = Ss + F2 * RS;                   // dy2 (same padded layout)
-    float* DP = Dys + F2 * RS;                   // dp2 [F2][T1]
-    float* red = sm;                             // NWAVE * 256, reused after the trial loop
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int li = lane & 15, lk = lane >> 4;
-
-    for (int i = tid; i < ((xdb ? 2 : 1) * C + 2 * F2) * RS; i += NTH) sm[i] = 0.f;
-    float aw[KS];
-    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
-    const int o = wave;
-    const bool row_on = o < F2;
-    const int oo = row_on ? o : 0;
-    float tap[K1];
-    {
-        const int gg = oo / g.D;
-#pragma unroll
-        for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + gg * K1 + k];
-    }
-    const float al = coef[CF_AL2 * CSTR + oo], be = coef[CF_BE2 * CSTR + oo];
-    const float ga = prm[g.o_g2 + oo], bt = prm[g.o_b2 + oo];
-    const float Ao = coef[CF_AO * CSTR + oo], Bo = coef[CF_BO * CSTR + oo], Co = coef[CF_CO * CSTR + oo];
-    // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] of this wave's row on the matrix
-    // cores (lagcorr_mfma); the tiles stay in registers for the whole workgroup
-    constexpr int NTQ = (K1 + 16) / 16;
-    floatx4 qacc[NTQ];
-#pragma unroll
-    for (int i = 0; i < NTQ; ++i) qacc[i] = (floatx4){0.f, 0.f, 0.f, 0.f};
-    float sdy = 0.f, sdyv = 0.f;
-    // dws GEMM split: wave -> (c-tile ct, k-group range)
-    const int wpc = NWAVE / NCT;
-    const bool gemm_on = wave < wpc * NCT;
-    const int ct = gemm_on ? wave / wpc : 0, part_ = gemm_on ? wave - ct * wpc : 0;
-    const int kg0 = (NT16 * part_) / wpc, kg1 = gemm_on ? (NT16 * (part_ + 1)) / wpc : 0;
-    floatx4 xacc = {0.f, 0.f, 0.f, 0.f};
-    float pf[PF];
-    // dp2 rows of the next trial ride along with its x (one trial ahead, registers): a synchronous
-    // load here would wait (vmcnt is in order) for the whole x prefetch issued before it
-    constexpr int NDP = (CC && TT) ? (FF * (TT / 4) + NTH - 1) / NTH : 4;   // F2 * T1 <= NDP * NTH
-    const int ndp = F2 * T1;
-    float pdp[NDP];
-    if ((int)blockIdx.x < g.B) {
-        x_prefetch<PF>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
-        for (int i = tid; i < ndp; i += NTH) DP[i] = dp2g[(size_t)blockIdx.x * ndp + i];
-    }
-    __syncthreads();
-    x_store<PF>(pf, C, T, RS, LP, Xb0, tid);
-    __syncthreads();
-
-    int it = 0;
-    TRACE(g, 4, TR_PRO);
-    TRACE_DECL();
-    drain_prologue_loads();
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x, ++it) {
-        const float* Xc = (it & 1) ? Xb1 : Xb0;
-        float* Xn = (it & 1) ? Xb0 : Xb1;
-        const int bn = b + gridDim.x;
-        if (bn < g.B) {
-            x_prefetch<PF>(x + (size_t)bn * C * T, C, T, pf, tid);
-#pragma unroll
-            for (int j = 0; j < NDP; ++j) {
-                const int i = tid + NTH * j;
-                if (i < ndp) pdp[j] = dp2g[(size_t)bn * ndp + i];
-            }
-        }
-        #ifndef EXP_NO_SPAT
-        spatial_mfma<KS>(Xc, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
-#endif
-
-        TRACE_PH(g, 4, 0, tph_);
-        __syncthreads();                                   // Ss, DP complete
-        TRACE_PH(g, 4, 1, tph_);
-        if (row_on) {
-            const float* row = Ss + o * RS;
-            float* drow = Dys + o * RS + LP;
-            for (int q = lane; q < TQ; q += 64) {
-                float w[4 * G_::NW];
-                lds_window<G_::NW>(row + 4 * q, w);
-                float v[4];
-                fir4<K1, G_::OFF>(w, tap, v);
-                const float dpq = (q < T1) ? DP[o * T1 + q] * 0.25f : 0.f;
-                float dy[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float xh = fmaf(al, v[i], be);
-                    const float z = fmaf(ga, xh, bt);
-                    const float dz = dpq * elu_d(z);
-                    float d = fmaf(Ao, dz, fmaf(Co, xh, Bo));
-                    d = (4 * q + i < T) ? d : 0.f;
-                    dy[i] = d;
-                    sdy += d;
-                    sdyv = fmaf(d, v[i], sdyv);
-                }
-                lds_st4(drow + 4 * q, (floatx4){dy[0], dy[1], dy[2], dy[3]});
-            }
-            TRACE_PH(g, 4, 2, tph_);
-            wave_lds_fence();
-#ifndef EXP_NO_LAG
-            lagcorr_mfma<NTQ>(Dys + o * RS + LP, Ss + o * RS + LP, T, NT16, g.P, qacc, lane);
-#endif
-            wave_lds_fence();                              // s row consumed before e overwrites it
-            // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
-            const float* dyr = Dys + o * RS;
-            float* erow = Ss + o * RS + LP;
-            for (int q = lane; q < TQ; q += 64) {
-                float w[4 * G_::NW];
-                lds_window<G_::NW>(dyr + 4 * q, w);
-                float e[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float a = 0.f;
-#pragma unroll
-                    for (int m = 0; m < K1; ++m) a = fmaf(tap[K1 - 1 - m], w[G_::OFFD + i + m], a);
-                    e[i] = (4 * q + i < T) ? a : 0.f;
-                }
-                lds_st4(erow + 4 * q, (floatx4){e[0], e[1], e[2], e[3]});
-            }
-        }
-        TRACE_PH(g, 4, 3, tph_);
-        if (xdb && bn < g.B) x_store<PF>(pf, C, T, RS, LP, Xn, tid);
-        TRACE_PH(g, 4, 4, tph_);
-        __syncthreads();                                   // e rows complete, Xn staged
-        TRACE_PH(g, 4, 5, tph_);
-        // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
-        // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
-#ifdef EXP_NO_DWS
-        if (false) {
-#else
-        if (gemm_on) {
-#endif
-            const int c = ct * 16 + li;
-            const float* arow = Ss + (li < F2 ? li : 0) * RS + LP + 4 * lk;
-            const float* brow = Xc + (c < C ? c : 0) * RS + LP + 4 * lk;
-            const bool aon = li < F2, bon = c < C;
-            for (int kg = kg0; kg < kg1; ++kg) {
-                floatx4 a4 = lds_ld4(arow + 16 * kg);
-                floatx4 b4 = lds_ld4(brow + 16 * kg);
-                if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
-            }
-        }
-        if (bn < g.B) {                            // next trial's dp2 rows: every FIR reader is past
-#pragma unroll
-            for (int j = 0; j < NDP; ++j) {
-                const int i = tid + NTH * j;
-                if (i < ndp) DP[i] = pdp[j];
-            }
-        }
-        TRACE_PH(g, 4, 6, tph_);
-        __syncthreads();                                   // e rows consumed before the next s
-        TRACE_PH(g, 4, 7, tph_);
-        if (!xdb && bn < g.B) {
-            x_store<PF>(pf, C, T, RS, LP, Xn, tid);
-            __syncthreads();
-        }
-    }
-    TRACE_LOOP(g, 4);
-    __syncthreads();
-
-    // ---- reductions ----
-    float* row = part + (size_t)blockIdx.x * g.nE;
-    {
-        float rv[4] = {sdy, sdyv, 0.f, 0.f};
-        wave_reduce<4>(rv);                              // lane 0: sum dy, lane 16: sum dy v
-        if (row_on && (lane == 0 || lane == 16))
-            pub(row + (F2 * K1 + F2 * C + (lane ? F2 : 0) + o), rv[0]);
-    }
-    // Q[o][k] = sum_i M_o[i][i+k] from this wave's lag-correlation tiles (LDS after the Xm slab)
-    float* Ms = red + NWAVE * 256;                   // [NWAVE][16][16 NTQ]
-#pragma unroll
-    for (int nt = 0; nt < NTQ; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Ms[(wave * 16 + 4 * lk + r) * (16 * NTQ) + 16 * nt + li] = qacc[nt][r];
-    // Xm: wave -> 16x16 tile partial (rows 4lk+r, col li) -> LDS [wave][256] -> sum over the
-    // waves of each c-tile
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave * 256 + (4 * lk + r) * 16 + li] = gemm_on ? xacc[r] : 0.f;
-    __syncthreads();
-    for (int p = tid; p < F2 * C; p += NTH) {
-        const int oo2 = p / C, c = p - oo2 * C;
-        const int ct2 = c >> 4, cc = c & 15;
-        float a = 0.f;
-        for (int w = ct2 * wpc; w < (ct2 + 1) * wpc; ++w) a += red[w * 256 + oo2 * 16 + cc];
-        pub(row + (F2 * K1 + p), a);
-    }
-    for (int p = tid; p < F2 * K1; p += NTH) {
-        const int oo2 = p / K1, k = p - oo2 * K1;
-        const float* Mo = Ms + oo2 * 16 * (16 * NTQ);
-        float a = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) a += Mo[i * (16 * NTQ) + i + k];
-        pub(row + p, a);
-    }
-    double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nE, fa, dsm)) { fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa); TRACE(g, 4, TR_FIN); }
 }
 
 // ================================================================================================

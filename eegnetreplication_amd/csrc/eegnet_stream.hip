@@ -1,0 +1,724 @@
+// eegnet_stream.hip -- the three passes that stream x (full-rate [C, T] trials): A (BN1 / BN2
+// batch statistics), B (forward to the pooled block-2 input, BN3 statistics) and E (dy2 and the
+// weight gradients that need full-rate data).  Included by eegnet_kernels.hip (one translation unit).
+//
+// Workgroup = 512 threads = 8 waves, two workgroups per CU (each <= 80 KB of LDS), trials strided
+// over the grid.  Wave w owns rows o = 2w, 2w+1 of every per-trial [F2, T] plane (F2 <= 16; with
+// EEGNet's D = 2 both rows share one temporal filter), so FIR taps are wave-uniform, the FIR windows
+// it reads are lane-contiguous float4s and its per-row partial sums stay in registers until the
+// workgroup ends.  The two workgroups of a CU run different trials and drift out of phase, so one's
+// MFMA / LDS / barrier phases overlap the other's VALU FIR work -- with one 16-wave workgroup per
+// CU every SIMD ran the same phase at the same time and the matrix and vector pipes took turns.
+
+namespace eeg {
+
+constexpr int NTB = 512;               // threads per workgroup of the streaming passes
+constexpr int NWB = NTB / 64;          // waves per workgroup
+constexpr int RPW = F2MAX / NWB;       // rows per wave (2)
+constexpr int WGPC = 2;                // workgroups per CU
+constexpr int WPEB = NWB * WGPC / 4;   // waves per SIMD: HIP's __launch_bounds__ second argument is
+                                       // the minimum waves per execution unit (caps VGPRs at 128)
+
+// FIR work layout: half-wave h = lane >> 5 takes row 2w + h, its 32 lanes take 8 consecutive
+// samples each (octet oc = (lane & 31) + 32 m): both rows of a wave advance together, with two
+// independent 4-output chains per lane per window load.
+#define EEG_NO(TT) ((TT) ? ((TT) + 7) / 8 : ((T + 7) >> 3))
+#define EEG_MO(TT) ((TT) ? (((TT) + 7) / 8 + 31) / 32 : 4)
+
+// x staging by LDS-DMA (global_load_lds_dwordx4: no VGPR destination, the wave's 64 lanes write
+// 1 KiB contiguously): one wave-instruction per 256-sample piece of a channel row, rows dealt
+// round-robin over the waves.  Used when T is a multiple of 256 (16-byte aligned, whole pieces);
+// other shapes stage through registers (x_prefetch / x_store).  The DMA is issued right after the
+// last reader of the x buffer and drains at the next __syncthreads() (the compiler's vmcnt(0)).
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+__device__ __forceinline__ void x_dma(const float* __restrict__ xb, int C, int T, int RS, int LP, float* Xs,
+                                      int wave, int lane) {
+    const int np = T >> 8;                             // 256-sample pieces per row
+    for (int i = wave; i < C * np; i += NWB) {
+        const int c = i / np, p = i - c * np;
+        __builtin_amdgcn_global_load_lds((gvoid_t*)(xb + (size_t)c * T + 256 * p + 4 * lane),
+                                         (lvoid_t*)(Xs + c * RS + LP + 256 * p), 16, 0, 0);
+    }
+}
+
+// this half-wave's taps (a per-lane select only when the two rows of a wave use different filters)
+template <int K1, int NTS>
+__device__ __forceinline__ void half_taps(const float (&tap)[NTS][K1], int hr, float (&tl)[K1]) {
+#pragma unroll
+    for (int k = 0; k < K1; ++k) tl[k] = hr ? tap[NTS - 1][k] : tap[0][k];
+}
+
+// Temporal taps of this wave's rows: one shared set for the specialised EEGNet-8,2 shapes (the
+// rows 2w, 2w+1 of a wave are group w when D = 2), one set per row otherwise.
+template <int K1, int NTS>
+__device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict__ prm, int D, int F2, int wave,
+                                          float (&tap)[NTS][K1]) {
+#pragma unroll
+    for (int r = 0; r < NTS; ++r) {
+        const int o = RPW * wave + r;
+        const int gg = (o < F2 ? o : 0) / D;
+#pragma unroll
+        for (int k = 0; k < K1; ++k) tap[r][k] = prm[g.o_w1 + gg * K1 + k];
+    }
+}
+
+// ================================================================================================
+// Pass A: BN1 / BN2 batch statistics (model.py:32, 47).
+// part row: [G0 K1][S0][H nH][Tl nTl][hs R][ts P][Sv F2][Sv2 F2]
+//   G0[d] = sum_{c,t<T} X[t] X[t+d]       (lag-Gram of the padded rows, window start 0)
+//   H[a,b] = sum_c x[a] x[b], 0<=a<=b<R    (head outer products -> Gram edge corrections)
+//   Tl[u,v] = sum_c x[T-P+u] x[T-P+v]     (tail outer products)
+//   hs / ts = head / tail sample sums       (window-sum corrections)
+//   Sv, Sv2 = sum v, sum v^2 per row o      (BN2: y2 = a1 v + c1 W)
+// ================================================================================================
+template <int K1, int CC, int TT, int FF>
+__global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __restrict__ prm,
+                                                      const float* __restrict__ x, float* __restrict__ part,
+                                                      FinArgs fa) {
+    using G_ = KG<K1>;
+    EEG_DIMS_NT(g, NTB);
+    TRACE(g, 0, TR_ENTRY);
+    // every pass re-arms its own tickets when it finishes; pass A also clears those of the later
+    // passes of this call (stream order), so a call never depends on how the previous one ended
+    if (blockIdx.x == 0 && threadIdx.x < (TK_PASSES - 1) * NCNT)
+        __hip_atomic_store(fa.cnt + NCNT + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    constexpr int NTS = FF ? 1 : RPW;
+    constexpr int NEI = G_::template nei<NTB>();
+    const int D = FF ? 2 : g.D;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const Xb = sm;              // one x buffer: the next trial lands after its last reader
+    float* Ss = sm + C * RS;
+    float* red = Ss + F2 * RS;                        // NWB * (K1 + 1)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    for (int i = tid; i < (C + F2) * RS; i += NTB) sm[i] = 0.f;
+    float aw[KS];
+    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
+    float tap[NTS][K1];
+    load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
+    const int NO = EEG_NO(TT);
+    float svl = 0.f, sv2l = 0.f;                     // this lane's row (half-wave) sums of v, v^2
+    float G0[K1];
+#pragma unroll
+    for (int d = 0; d < K1; ++d) G0[d] = 0.f;
+    float s0 = 0.f;
+    // edge items: decode (row-index a, row-index b) once; b < 0 -> a plain sample sum
+    float eacc[NEI];
+    int ea[NEI], eb[NEI];
+#pragma unroll
+    for (int i = 0; i < NEI; ++i) {
+        eacc[i] = 0.f;
+        int e = tid + NTB * i;
+        ea[i] = -1; eb[i] = -1;
+        if (e < g.nH) {                                  // head pair (a <= b < R), a-major
+            int a = 0;
+            while (e >= g.R - a) { e -= g.R - a; ++a; }
+            ea[i] = a; eb[i] = a + e;
+        } else if ((e -= g.nH) < g.nTl) {                // tail pair (u <= v < P)
+            int u = 0;
+            while (e >= g.P - u) { e -= g.P - u; ++u; }
+            ea[i] = T - g.P + u; eb[i] = T - g.P + u + e;
+        } else if ((e -= g.nTl) < g.R) {
+            ea[i] = e;
+        } else if ((e -= g.R) < g.P) {
+            ea[i] = T - g.P + e;
+        } else {
+            ea[i] = -2;                                  // unused slot
+        }
+    }
+    constexpr bool XDMA = TT && (TT % 256 == 0);
+    float pf[XDMA ? 1 : PF];
+    if constexpr (XDMA) {
+        __syncthreads();                                 // the zero fill precedes the DMA writes
+        if ((int)blockIdx.x < g.B) x_dma(x + (size_t)blockIdx.x * C * T, C, T, RS, LP, Xb, wave, lane);
+        __syncthreads();
+    } else {
+        if ((int)blockIdx.x < g.B) x_prefetch<PF, NTB>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
+        __syncthreads();
+        x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+        __syncthreads();
+    }
+
+    TRACE(g, 0, TR_PRO);
+    TRACE_DECL();
+    drain_prologue_loads();
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+        const int bn = b + gridDim.x;
+        if constexpr (!XDMA)
+            if (bn < g.B) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
+        spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+        // lag-Gram: items (c, quad), lanes of a wave on consecutive quads of one row
+        for (int j = tid; j < C * TQ; j += NTB) {
+            const int c = j / TQ, q = j - c * TQ;
+            float w[4 * G_::NW];
+            lds_window<G_::NW>(Xb + c * RS + 4 * q, w);
+            float a[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = (4 * q + i < T) ? w[G_::OFF + i] : 0.f;
+            s0 += (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+            for (int d = 0; d < K1; ++d) {
+                float acc = G0[d];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = fmaf(a[i], w[G_::OFF + i + d], acc);
+                G0[d] = acc;
+            }
+        }
+        // edge outer products / sums over channels
+#pragma unroll
+        for (int i = 0; i < NEI; ++i) {
+            if (ea[i] >= 0) {
+                const float* xa = Xb + LP + ea[i];
+                float acc0 = 0.f, acc1 = 0.f;
+                if (eb[i] >= 0) {
+                    const float* xb2 = Xb + LP + eb[i];
+                    int c = 0;
+                    for (; c + 1 < C; c += 2) {
+                        acc0 = fmaf(xa[c * RS], xb2[c * RS], acc0);
+                        acc1 = fmaf(xa[(c + 1) * RS], xb2[(c + 1) * RS], acc1);
+                    }
+                    if (c < C) acc0 = fmaf(xa[c * RS], xb2[c * RS], acc0);
+                } else {
+                    int c = 0;
+                    for (; c + 1 < C; c += 2) { acc0 += xa[c * RS]; acc1 += xa[(c + 1) * RS]; }
+                    if (c < C) acc0 += xa[c * RS];
+                }
+                eacc[i] += acc0 + acc1;
+            }
+        }
+        TRACE_PH(g, 0, 0, tph_);
+        __syncthreads();                                   // Ss complete, x read for good
+        if constexpr (XDMA)
+            if (bn < g.B) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+        TRACE_PH(g, 0, 1, tph_);
+        // v = 32-tap FIR of this wave's s rows; BN2 sums of v
+        {
+            const int hr = lane >> 5, o = RPW * wave + hr;
+            float tl[K1];
+            half_taps<K1, NTS>(tap, hr, tl);
+            if (o < F2) {
+                const float* row = Ss + o * RS;
+                for (int oc = lane & 31; oc < NO; oc += 32) {
+                    float w[4 * G_::NW8];
+                    lds_window<G_::NW8>(row + 8 * oc, w);
+                    float v[8];
+                    fir8<K1, G_::OFF>(w, tl, v);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
+                }
+            }
+        }
+        TRACE_PH(g, 0, 2, tph_);
+        if constexpr (!XDMA)
+            if (bn < g.B) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+        TRACE_PH(g, 0, 3, tph_);
+        __syncthreads();                                   // Xb staged, Ss free
+        TRACE_PH(g, 0, 4, tph_);
+    }
+    TRACE_LOOP(g, 0);
+
+    // ---- workgroup reduction -> one partial row ----
+    float* row = part + (size_t)blockIdx.x * g.nA;
+    {
+        constexpr int NR = K1 + 8, NQ = NR / 4;       // [G0 K1][s0][sv RPW][sv2 RPW][pad]
+        float rv[NR];
+#pragma unroll
+        for (int d = 0; d < K1; ++d) rv[d] = G0[d];
+        rv[K1] = s0;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            rv[K1 + 1 + r] = (lane >> 5) == r ? svl : 0.f;
+            rv[K1 + 1 + RPW + r] = (lane >> 5) == r ? sv2l : 0.f;
+        }
+#pragma unroll
+        for (int i = K1 + 1 + 2 * RPW; i < NR; ++i) rv[i] = 0.f;
+        wave_reduce<NR>(rv);
+        if ((lane & 15) == 0) {
+            const int r0 = (lane >> 4) * NQ;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                const int idx = j + r0;
+                if (idx <= K1) {
+                    red[wave * (K1 + 1) + idx] = rv[j];
+                } else if (idx < K1 + 1 + 2 * RPW) {
+                    const int k = idx - K1 - 1, r = k % RPW, o = RPW * wave + r;
+                    if (o < F2) pub(row + (K1 + 1 + g.nedge + (k < RPW ? 0 : F2) + o), rv[j]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (tid <= K1) {
+        float t = 0.f;
+        for (int w = 0; w < NWB; ++w) t += red[w * (K1 + 1) + tid];
+        pub(row + (tid), t);
+    }
+#pragma unroll
+    for (int i = 0; i < NEI; ++i)
+        if (ea[i] != -2 && tid + NTB * i < g.nedge) pub(row + (K1 + 1 + tid + NTB * i), eacc[i]);
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nA, fa, dsm)) { fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa); TRACE(g, 0, TR_FIN); }
+}
+
+// ================================================================================================
+// Pass B: forward to d2, E1/E2 (pooled ELU' sums for the BN2 backward), BN3 statistics.
+// part row: [Sr F2][Sr2 F2]
+// LDS: x rows | s rows | d2 rows (pad LP2) | q rows | weight table [w2 F2MAX x 16][W3 F2MAX x F2MAX]
+// ================================================================================================
+template <int K1, int CC, int TT, int FF>
+__global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __restrict__ prm,
+                                                      const float* coef,    // the finalize writes it: no __restrict__
+                                                      const float* __restrict__ x,
+                                                      const uint8_t* __restrict__ mask2,
+                                                      float* __restrict__ d2g, float* __restrict__ E1g,
+                                                      float* __restrict__ E2g, float* __restrict__ part,
+                                                      FinArgs fa) {
+    using G_ = KG<K1>;
+    EEG_DIMS_NT(g, NTB);
+    TRACE(g, 1, TR_ENTRY);
+    constexpr int NTS = FF ? 1 : RPW;
+    const int D = FF ? 2 : g.D;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const Xb = sm;              // one x buffer: the next trial lands after its last reader
+    float* Ss = sm + C * RS;
+    float* D2s = Ss + F2 * RS;
+    float* Qs = D2s + F2 * RS2;
+    float* Wt = Qs + F2 * RS2;         // block-2 weights, read with wave-uniform addresses
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    for (int i = tid; i < (C + F2) * RS + 2 * F2 * RS2; i += NTB) sm[i] = 0.f;
+    for (int i = tid; i < F2MAX * (K2 + F2MAX); i += NTB) {
+        float v = 0.f;
+        if (i < F2MAX * K2) { if (i < F2 * K2) v = prm[g.o_w2 + i]; }
+        else {
+            const int j = (i - F2MAX * K2) / F2MAX, c = (i - F2MAX * K2) % F2MAX;
+            if (j < F2 && c < F2) v = prm[g.o_W3 + j * F2 + c];
+        }
+        Wt[i] = v;
+    }
+    float aw[KS];
+    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
+    float tap[NTS][K1];
+    load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
+    const int NO = EEG_NO(TT);
+    float sr[RPW], sr2[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) { sr[r] = 0.f; sr2[r] = 0.f; }
+    // BN2 constants of this lane's FIR row (half-wave hr = lane >> 5)
+    float alh, beh, gah, bth;
+    {
+        const int o = RPW * wave + (lane >> 5), oo = o < F2 ? o : 0;
+        alh = coef[CF_AL2 * CSTR + oo]; beh = coef[CF_BE2 * CSTR + oo];
+        gah = prm[g.o_g2 + oo]; bth = prm[g.o_b2 + oo];
+    }
+    constexpr bool XDMA = TT && (TT % 256 == 0);
+    float pf[XDMA ? 1 : PF];
+    if constexpr (XDMA) {
+        __syncthreads();                                 // the zero fill precedes the DMA writes
+        if ((int)blockIdx.x < g.B) x_dma(x + (size_t)blockIdx.x * C * T, C, T, RS, LP, Xb, wave, lane);
+        __syncthreads();
+    } else {
+        if ((int)blockIdx.x < g.B) x_prefetch<PF, NTB>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
+        __syncthreads();
+        x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+        __syncthreads();
+    }
+
+    TRACE(g, 1, TR_PRO);
+    TRACE_DECL();
+    drain_prologue_loads();
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+        const int bn = b + gridDim.x;
+        if constexpr (!XDMA)
+            if (bn < g.B) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
+        spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+        TRACE_PH(g, 1, 0, tph_);
+        __syncthreads();                                   // Ss complete; Qs free; x read for good
+        if constexpr (XDMA)
+            if (bn < g.B) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+        TRACE_PH(g, 1, 1, tph_);
+        // d2 / E1 / E2 stay in registers until the next trial's x is staged: a global store issued
+        // before that x_store would hold its vmcnt wait (loads and stores drain in order)
+        constexpr int MO = EEG_MO(TT);
+        float d2v[MO][2], e1v[MO][2], e2v[MO][2];
+        const int hr = lane >> 5, oh = RPW * wave + hr;
+        {
+            float tl[K1];
+            half_taps<K1, NTS>(tap, hr, tl);
+            if (oh < F2) {
+                const float* row = Ss + oh * RS;
+                float* drow = D2s + oh * RS2 + LP2;
+#pragma unroll
+                for (int m = 0; m < MO; ++m) {
+                    const int oc = (lane & 31) + 32 * m;
+                    if (oc >= NO) break;
+                    float w[4 * G_::NW8];
+                    lds_window<G_::NW8>(row + 8 * oc, w);
+                    float v[8];
+                    fir8<K1, G_::OFF>(w, tl, v);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {                // the octet's two pool-4 windows
+                        const int q = 2 * oc + h;
+                        float pe = 0.f, e1 = 0.f, e2 = 0.f;
+#pragma unroll
+                        for (int i = 4 * h; i < 4 * h + 4; ++i) {
+                            const float xh = fmaf(alh, v[i], beh);
+                            const float z = fmaf(gah, xh, bth);
+                            const float dz = elu_d(z);
+                            pe += z > 0.f ? z : dz - 1.f;          // ELU(z) = exp(z) - 1 below 0
+                            e1 += dz;
+                            e2 = fmaf(dz, xh, e2);
+                        }
+                        const float d2 = q < T1 ? pe * 0.25f * keep_mul(g, mask2, 0, (unsigned)((b * F2 + oh) * T1 + q)) : 0.f;
+                        d2v[m][h] = d2; e1v[m][h] = e1; e2v[m][h] = e2;
+                        if (q < T1) drow[q] = d2;
+                    }
+                }
+            }
+        }
+        wave_lds_fence();
+        // depthwise 1x16 'same' conv of this wave's rows (model.py:54-61): pad 7 | 8
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int o = RPW * wave + r;
+            if (o < F2) {
+                const float* dr = D2s + o * RS2 + LP2 - 7;
+                const float* w2 = Wt + o * K2;
+                for (int t = lane; t < T1; t += 64) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int k = 0; k < K2; ++k) a = fmaf(w2[k], dr[t + k], a);
+                    Qs[o * RS2 + t] = a;
+                }
+            }
+        }
+        TRACE_PH(g, 1, 2, tph_);
+        if constexpr (!XDMA)
+            if (bn < g.B) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+        if (oh < F2) {
+#pragma unroll
+            for (int m = 0; m < MO; ++m) {
+                const int oc = (lane & 31) + 32 * m;
+                if (oc >= NO) break;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int q = 2 * oc + h;
+                    if (q < T1) {
+                        const size_t gi = ((size_t)b * F2 + oh) * T1 + q;
+                        d2g[gi] = d2v[m][h]; E1g[gi] = e1v[m][h]; E2g[gi] = e2v[m][h];
+                    }
+                }
+            }
+        }
+        TRACE_PH(g, 1, 3, tph_);
+        __syncthreads();                                   // Qs complete, Xb staged
+        TRACE_PH(g, 1, 4, tph_);
+        // pointwise F2 x F2 (model.py:62-69) for this wave's rows; BN3 sums
+        for (int t = lane; t < T1; t += 64) {
+            float qv[F2MAX];
+#pragma unroll
+            for (int i = 0; i < F2MAX; ++i) qv[i] = i < F2 ? Qs[i * RS2 + t] : 0.f;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int o = RPW * wave + r;
+                if (o < F2) {
+                    const float* w3 = Wt + F2MAX * K2 + o * F2MAX;
+                    float rr = 0.f;
+#pragma unroll
+                    for (int i = 0; i < F2MAX; ++i) rr = fmaf(w3[i], qv[i], rr);
+                    sr[r] += rr;
+                    sr2[r] = fmaf(rr, rr, sr2[r]);
+                }
+            }
+        }
+        TRACE_PH(g, 1, 5, tph_);
+    }
+    TRACE_LOOP(g, 1);
+    {
+        float rv[4] = {sr[0], sr[1], sr2[0], sr2[1]};
+        wave_reduce<4>(rv);                        // lane 16k: item k = (k < 2 ? sr : sr2)[k % 2]
+        const int k = lane >> 4, o = RPW * wave + (k & 1);
+        if ((lane & 15) == 0 && o < F2) {
+            float* row = part + (size_t)blockIdx.x * g.nB;
+            pub(row + ((k < 2 ? 0 : F2) + o), rv[0]);
+        }
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nB, fa, dsm)) { fin2(g, dsm + 2, fa); TRACE(g, 1, TR_FIN); }
+}
+
+// ================================================================================================
+// Pass E: dy2 and the weight-gradient reductions that need full-rate data.
+// part row: [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2]
+// LDS: x rows | s rows, then e | dy rows | dp2 [F2][T1]; after the loop: dws tiles | lag tiles
+// ================================================================================================
+template <int K1, int CC, int TT, int FF>
+__global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,   // Adam (finalize) writes it
+                                                      const float* coef,    // the finalize writes it: no __restrict__
+                                                      const float* __restrict__ x,
+                                                      const float* __restrict__ dp2g,
+                                                      float* __restrict__ part, FinArgs fa) {
+    using G_ = KG<K1>;
+    EEG_DIMS_NT(g, NTB);
+    TRACE(g, 4, TR_ENTRY);
+    constexpr int NTS = FF ? 1 : RPW;
+    const int D = FF ? 2 : g.D;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const Xb = sm;
+    float* Ss = sm + C * RS;                     // s, then e
+    float* Dys = Ss + F2 * RS;                   // dy2 (same padded layout)
+    float* DP = Dys + F2 * RS;                   // dp2 [F2][T1]
+    float* red = sm;                             // NWB * 256 dws tiles, reused after the trial loop
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+
+    for (int i = tid; i < (C + 2 * F2) * RS; i += NTB) sm[i] = 0.f;
+    float aw[KS];
+    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
+    float tap[NTS][K1];
+    load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
+    // BN2 forward / backward constants of this lane's row (half-wave hr = lane >> 5)
+    float alh, beh, gah, bth, Aoh, Boh, Coh;
+    {
+        const int o = RPW * wave + (lane >> 5), oo = o < F2 ? o : 0;
+        alh = coef[CF_AL2 * CSTR + oo]; beh = coef[CF_BE2 * CSTR + oo];
+        gah = prm[g.o_g2 + oo]; bth = prm[g.o_b2 + oo];
+        Aoh = coef[CF_AO * CSTR + oo]; Boh = coef[CF_BO * CSTR + oo]; Coh = coef[CF_CO * CSTR + oo];
+    }
+    const int NO = EEG_NO(TT);
+    float sdyl = 0.f, sdyvl = 0.f;                   // this lane's row (half-wave) sums of dy, dy v
+    // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] of this lane's row, accumulated
+    // from the FIR's own s window (VALU: the f32 MFMA shares the vector pipe and its row-block
+    // formulation would cost 1.5x the MACs)
+    float Q[K1];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) Q[k] = 0.f;
+    // dws GEMM split: wave -> (c-tile ct, k-group range)
+    const int wpc = NWB / NCT;
+    const bool gemm_on = wave < wpc * NCT;
+    const int ct = gemm_on ? wave / wpc : 0, part_ = gemm_on ? wave - ct * wpc : 0;
+    const int kg0 = (NT16 * part_) / wpc, kg1 = gemm_on ? (NT16 * (part_ + 1)) / wpc : 0;
+    floatx4 xacc = {0.f, 0.f, 0.f, 0.f};
+    constexpr bool XDMA = TT && (TT % 256 == 0);
+    float pf[XDMA ? 1 : PF];
+    // dp2 rows of the next trial ride along (registers, one trial ahead): a synchronous load would
+    // wait (vmcnt is in order) for every memory operation issued before it
+    constexpr int NDP = (CC && TT) ? (FF * (TT / 4) + NTB - 1) / NTB : 8;   // F2 * T1 <= NDP * NTB
+    const int ndp = F2 * T1;
+    float pdp[NDP];
+    // with LDS-DMA staging the dws GEMM reads its x operand straight from global memory (L2-warm:
+    // the same trial's x was just DMA'd), so the x buffer is free right after the spatial GEMM and
+    // the next trial's DMA overlaps the whole FIR / FIR^T phase
+    constexpr int NKGW = XDMA ? (TT / 16 + NWB / ((CC + 15) / 16) - 1) / (NWB / ((CC + 15) / 16)) : 1;
+    floatx4 xg[NKGW];
+    if constexpr (XDMA) {
+        __syncthreads();                                 // the zero fill precedes the DMA writes
+        if ((int)blockIdx.x < g.B) {
+            x_dma(x + (size_t)blockIdx.x * C * T, C, T, RS, LP, Xb, wave, lane);
+            for (int i = tid; i < ndp; i += NTB) DP[i] = dp2g[(size_t)blockIdx.x * ndp + i];
+        }
+        __syncthreads();
+    } else {
+        if ((int)blockIdx.x < g.B) {
+            x_prefetch<PF, NTB>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
+            for (int i = tid; i < ndp; i += NTB) DP[i] = dp2g[(size_t)blockIdx.x * ndp + i];
+        }
+        __syncthreads();
+        x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+        __syncthreads();
+    }
+
+    TRACE(g, 4, TR_PRO);
+    TRACE_DECL();
+    drain_prologue_loads();
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+        const int bn = b + gridDim.x;
+        spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+        TRACE_PH(g, 4, 0, tph_);
+        __syncthreads();                                   // Ss, DP complete
+        if constexpr (XDMA)
+            if (bn < g.B) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+        TRACE_PH(g, 4, 1, tph_);
+        {
+            const int hr = lane >> 5, oh = RPW * wave + hr;
+            float tl[K1];
+            half_taps<K1, NTS>(tap, hr, tl);
+            if (oh < F2) {
+                const float* row = Ss + oh * RS;
+                float* drow = Dys + oh * RS + LP;
+                for (int oc = lane & 31; oc < NO; oc += 32) {
+                    float w[4 * G_::NW8];
+                    lds_window<G_::NW8>(row + 8 * oc, w);
+                    float v[8];
+                    fir8<K1, G_::OFF>(w, tl, v);
+                    float dpq[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) dpq[h] = (2 * oc + h < T1) ? DP[oh * T1 + 2 * oc + h] * 0.25f : 0.f;
+                    float dy[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const float xh = fmaf(alh, v[i], beh);
+                        const float z = fmaf(gah, xh, bth);
+                        const float dz = dpq[i >> 2] * elu_d(z);
+                        float d = fmaf(Aoh, dz, fmaf(Coh, xh, Boh));
+                        d = (8 * oc + i < T) ? d : 0.f;
+                        dy[i] = d;
+                        sdyl += d;
+                        sdyvl = fmaf(d, v[i], sdyvl);
+                    }
+                    // Q[k] += sum_i dy[t0+i] s[t0+i+k-P]
+#pragma unroll
+                    for (int k = 0; k < K1; ++k)
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) Q[k] = fmaf(dy[i], w[G_::OFF + i + k], Q[k]);
+                    lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
+                    lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
+                }
+            }
+            wave_lds_fence();                              // dy rows complete; s rows consumed
+            // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
+            if (oh < F2) {
+                const float* dyr = Dys + oh * RS;
+                float* erow = Ss + oh * RS + LP;
+                for (int oc = lane & 31; oc < NO; oc += 32) {
+                    float w[4 * G_::NW8];
+                    lds_window<G_::NW8>(dyr + 8 * oc, w);
+                    float e[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) e[i] = 0.f;
+#pragma unroll
+                    for (int m = 0; m < K1; ++m)
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) e[i] = fmaf(tl[K1 - 1 - m], w[G_::OFFD + i + m], e[i]);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
+                    lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
+                    lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+                }
+            }
+        }
+        TRACE_PH(g, 4, 2, tph_);
+        // the next trial's dp2 is fetched here, its x after the GEMM: their registers must not be
+        // live across the FIR / FIR^T phase (the kernel's register peak, 128 VGPRs at 4 waves/SIMD);
+        // the other workgroup on the CU covers the exposed latency
+        if (bn < g.B) {
+#pragma unroll
+            for (int j = 0; j < NDP; ++j) {
+                const int i = tid + NTB * j;
+                if (i < ndp) pdp[j] = dp2g[(size_t)bn * ndp + i];
+            }
+        }
+        if constexpr (XDMA) {                              // this trial's x operand of the dws GEMM
+            const int c = ct * 16 + li;
+            const float* xr = x + ((size_t)b * C + (c < C ? c : 0)) * T + 4 * lk;
+#pragma unroll
+            for (int j = 0; j < NKGW; ++j) {
+                const int kg = kg0 + j;
+                xg[j] = (gemm_on && kg < kg1 && c < C) ? *reinterpret_cast<const floatx4*>(xr + 16 * kg)
+                                                      : (floatx4){0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        __syncthreads();                                   // e rows complete
+        TRACE_PH(g, 4, 3, tph_);
+        // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
+        // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
+        if (gemm_on) {
+            const int c = ct * 16 + li;
+            const float* arow = Ss + (li < F2 ? li : 0) * RS + LP + 4 * lk;
+            const bool aon = li < F2, bon = c < C;
+            if constexpr (XDMA) {
+#pragma unroll
+                for (int j = 0; j < NKGW; ++j) {
+                    const int kg = kg0 + j;
+                    if (kg < kg1) {
+                        floatx4 a4 = lds_ld4(arow + 16 * kg);
+                        if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                        const floatx4 b4 = xg[j];
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
+                    }
+                }
+            } else {
+                const float* brow = Xb + (c < C ? c : 0) * RS + LP + 4 * lk;
+                for (int kg = kg0; kg < kg1; ++kg) {
+                    floatx4 a4 = lds_ld4(arow + 16 * kg);
+                    floatx4 b4 = lds_ld4(brow + 16 * kg);
+                    if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                    if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
+                }
+            }
+        }
+        if (bn < g.B) {                            // next trial's dp2 rows: every FIR reader is past
+#pragma unroll
+            for (int j = 0; j < NDP; ++j) {
+                const int i = tid + NTB * j;
+                if (i < ndp) DP[i] = pdp[j];
+            }
+            if constexpr (!XDMA) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
+        }
+        TRACE_PH(g, 4, 4, tph_);
+        __syncthreads();                                   // x and e rows consumed
+        TRACE_PH(g, 4, 5, tph_);
+        if constexpr (!XDMA) {
+            if (bn < g.B) {
+                x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+                TRACE_PH(g, 4, 6, tph_);
+                __syncthreads();                           // next trial's x staged
+            }
+        }
+        TRACE_PH(g, 4, 7, tph_);
+    }
+    TRACE_LOOP(g, 4);
+    __syncthreads();
+
+    // ---- reductions ----
+    float* row = part + (size_t)blockIdx.x * g.nE;
+    {
+        // per-row (half-wave) sums: [Q K1][sdy][sdyv][pad 2]
+        constexpr int NR = K1 + 4, NH = NR / 2;
+        float rv[NR];
+#pragma unroll
+        for (int k = 0; k < K1; ++k) rv[k] = Q[k];
+        rv[K1] = sdyl; rv[K1 + 1] = sdyvl; rv[K1 + 2] = 0.f; rv[K1 + 3] = 0.f;
+        half_reduce<NR>(rv);
+        if ((lane & 15) == 0) {
+            const int o = RPW * wave + (lane >> 5), off = ((lane >> 4) & 1) * NH;
+            if (o < F2) {
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    const int idx = j + off;
+                    if (idx < K1) pub(row + (o * K1 + idx), rv[j]);
+                    else if (idx == K1) pub(row + (F2 * K1 + F2 * C + o), rv[j]);
+                    else if (idx == K1 + 1) pub(row + (F2 * K1 + F2 * C + F2 + o), rv[j]);
+                }
+            }
+        }
+    }
+    // Xm: wave -> 16x16 tile partial (rows 4lk+q, col li) -> LDS [wave][256] -> sum over the
+    // waves of each c-tile
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[wave * 256 + (4 * lk + q) * 16 + li] = gemm_on ? xacc[q] : 0.f;
+    __syncthreads();
+    for (int p = tid; p < F2 * C; p += NTB) {
+        const int oo2 = p / C, c = p - oo2 * C;
+        const int ct2 = c >> 4, cc = c & 15;
+        float a = 0.f;
+        for (int w = ct2 * wpc; w < (ct2 + 1) * wpc; ++w) a += red[w * 256 + oo2 * 16 + cc];
+        pub(row + (F2 * K1 + p), a);
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nE, fa, dsm)) { fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa); TRACE(g, 4, TR_FIN); }
+}
+
+}  // namespace eeg

@@ -89,9 +89,7 @@ class DataParallelTrainer:
         m = self.model
         ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
                        self.adam.grads, None, None, self.workspace(x.shape[0]), self.loss,
-                       clamp=False)
-        for bn in m._bns():
-            bn.num_batches_tracked.add_(1)
+                       clamp=False, nbt=m.flat_num_batches_tracked())
         return self.adam.grads
 
     def clamp(self, grads):

@@ -92,6 +92,14 @@ class EEGNet(nn.Module):
             bn.running_mean = rm
             bn.running_var = rv
         self._bn_flat = bflat
+        # the three num_batches_tracked counters as views of one int64[3] buffer: the HIP forward
+        # increments them in-kernel (no per-step host-side add_ launches)
+        nflat = torch.zeros(3, dtype=torch.int64, device=dev)
+        for i, bn in enumerate(self._bns()):
+            if bn.num_batches_tracked is not None:
+                nflat[i:i + 1].copy_(bn.num_batches_tracked.reshape(1))
+                bn.num_batches_tracked = nflat[i:i + 1].view(())
+        self._nbt_flat = nflat
 
     def _apply(self, fn, recurse=True):
         super()._apply(fn, recurse)
@@ -113,6 +121,10 @@ class EEGNet(nn.Module):
                 if t.data_ptr() != b + 4 * o:
                     return False
                 o += t.numel()
+        n = self._nbt_flat.data_ptr()
+        for i, bn in enumerate(self._bns()):
+            if bn.num_batches_tracked is not None and bn.num_batches_tracked.data_ptr() != n + 8 * i:
+                return False
         return True
 
     def flat_parameters(self) -> torch.Tensor:
@@ -124,6 +136,12 @@ class EEGNet(nn.Module):
         if not self._flat_ok():
             self._flatten()
         return self._bn_flat
+
+    def flat_num_batches_tracked(self) -> torch.Tensor:
+        """int64[3] device buffer behind the three BatchNorm2d.num_batches_tracked counters."""
+        if not self._flat_ok():
+            self._flatten()
+        return self._nbt_flat
 
     @property
     def shape(self) -> Shape:
@@ -181,10 +199,7 @@ class _TrainFn(torch.autograd.Function):
         ws = ops.new_workspace(shape, x.shape[0], x.device)
         flat = mod.flat_parameters().clone()
         logits = ops.forward_train(shape, flat, mod.flat_bn_buffers(), x, ws, seed, offset,
-                                   masks=masks)
-        for bn in mod._bns():
-            if bn.num_batches_tracked is not None:
-                bn.num_batches_tracked.add_(1)
+                                   masks=masks, nbt=mod.flat_num_batches_tracked())
         ctx.shape, ctx.seed, ctx.offset, ctx.masks = shape, seed, offset, masks
         ctx.param_shapes = [p.shape for p in params]
         ctx.save_for_backward(x, ws, flat)
@@ -310,9 +325,8 @@ class FusedTrainer:
         seed, offset = m.next_dropout_key()
         ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
                        self.adam.grads, self.adam.state, self.adam.step, self.workspace(x.shape[0]),
-                       self.loss, logits=logits, lr=self.lr, betas=self.betas, eps=self.eps)
-        for bn in m._bns():
-            bn.num_batches_tracked.add_(1)
+                       self.loss, logits=logits, lr=self.lr, betas=self.betas, eps=self.eps,
+                       nbt=m.flat_num_batches_tracked())
         return self.loss
 
 

@@ -91,11 +91,11 @@ class Shape:
 
 def new_workspace(shape: Shape, B: int, device) -> torch.Tensor:
     nbytes = _lib.workspace_bytes(shape.dims(B))
-    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+    return torch.zeros(nbytes, dtype=torch.uint8, device=device)   # zero-filled once (tickets)
 
 
 def forward_train(shape: Shape, flat_params, bn_flat, x, ws, seed: int, offset: int,
-                  masks=None, p: float | None = None) -> torch.Tensor:
+                  masks=None, p: float | None = None, nbt=None) -> torch.Tensor:
     """Train-mode forward: BN batch stats (+ running-stat update in bn_flat), dropout."""
     B = x.shape[0]
     logits = torch.empty((B, NCLS), dtype=torch.float32, device=x.device)
@@ -103,8 +103,8 @@ def forward_train(shape: Shape, flat_params, bn_flat, x, ws, seed: int, offset: 
     d = shape.dims(B, p)
     _lib.check(_lib.load().eegnet_forward_train(
         ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(m2), _ptr(m3),
-        ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(logits), _ptr(ws), _stream()),
-        "eegnet_forward_train")
+        ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(logits), _ptr(ws), _stream(),
+        _ptr(nbt)), "eegnet_forward_train")
     return logits
 
 
@@ -150,7 +150,7 @@ def adam_step(params, grads, exp_avg, exp_avg_sq, step_i32, lr=1e-3, betas=(0.9,
 
 def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset: int, grads,
                adam_state, step_i32, ws, loss, logits=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-7,
-               p: float | None = None, clamp=True):
+               p: float | None = None, clamp=True, nbt=None):
     """One fused hot-loop iteration (model.py:141-148) on the device, no host sync.
     ``adam_state=None`` stops after the gradients (data-parallel)."""
     d = shape.dims(x.shape[0], p)
@@ -159,4 +159,4 @@ def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset:
         ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),
         _ptr(step_i32), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
         ctypes.c_float(eps), _ptr(loss), _ptr(logits), _ptr(ws), _stream(),
-        0 if clamp else NO_CLAMP), "eegnet_train_step")
+        0 if clamp else NO_CLAMP, _ptr(nbt)), "eegnet_train_step")

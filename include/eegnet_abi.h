@@ -64,14 +64,19 @@ enum { EEGNET_NO_CLAMP = 1 /* leave model.py:44/84 clamps to eegnet_clamp_grads 
 /* Number of fp32 elements of the flat parameter buffer for these dims. */
 int eegnet_param_count(const eegnet_dims* dims, int64_t* out);
 
-/* Bytes of scratch the train-mode calls need (forward -> backward state lives here). */
+/* Bytes of scratch the train-mode calls need (forward -> backward state lives here).  The workspace
+ * must be zero-filled once before its first use (hipMemset / torch.zeros); the library keeps its
+ * reduction tickets re-armed from then on. */
 int eegnet_workspace_bytes(const eegnet_dims* dims, size_t* out);
 
 /* Train-mode forward (BN batch statistics, dropout, running-stat momentum update).
- * Replaces model.py:141 `preds = model(signals)` in train mode.  Leaves what backward needs in `ws`. */
+ * Replaces model.py:141 `preds = model(signals)` in train mode.  Leaves what backward needs in `ws`.
+ * num_batches_tracked (nullable): the three BatchNorm2d counters as one int64[3] device buffer,
+ * incremented in-kernel. */
 int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn_buffers,
                          const float* x, const uint8_t* mask2, const uint8_t* mask3,
-                         uint64_t seed, uint64_t offset, float* logits, void* ws, void* stream);
+                         uint64_t seed, uint64_t offset, float* logits, void* ws, void* stream,
+                         int64_t* num_batches_tracked);
 
 /* Backward of the last eegnet_forward_train on the same `ws` (same x, params, masks, seed/offset).
  * Gradient source: `dlogits` [B,4] if non-NULL (autograd), else mean cross-entropy against `labels`
@@ -104,7 +109,8 @@ int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_av
 int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers, const float* x,
                       const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
                       float* adam_state, int32_t* step, float lr, float beta1, float beta2,
-                      float eps, float* loss, float* logits, void* ws, void* stream, int flags);
+                      float eps, float* loss, float* logits, void* ws, void* stream, int flags,
+                      int64_t* num_batches_tracked);
 
 /* Optional per-kernel device timing for benchmarks: while enabled, every kernel this thread
  * launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect synchronises

@@ -46,14 +46,16 @@ def main():
     torch.cuda.synchronize()
     lib.eegnet_trace_enable(None)
     a = buf.cpu().numpy().reshape(8, MAXWG, SLOTS).astype(np.float64)
-    grid = int((a[0, :, 0] > 0).sum())
+    grids = [int((a[p, :, 0] > 0).sum()) for p in range(5)]
+    grid = grids[0]
     t0 = a[0, :grid, 0].min()
     us = lambda v: (v - t0) / 100.0   # 100 MHz wall clock -> µs from pass A's first entry
     prev_end = None
     ntr = max(1, args.batch // grid)
-    print(f"grid={grid} workgroups, {ntr} trials per workgroup")
+    print(f"grids {grids} workgroups")
     for p in range(5):
-        st = a[p, :grid]
+        st = a[p, :grids[p]]
+        ntr = max(1, args.batch // grids[p])
         ent, pro, loop, pub = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
         grp = st[:, 4][st[:, 4] > 0]
         top = st[:, 5][st[:, 5] > 0]
