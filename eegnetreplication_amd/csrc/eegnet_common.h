@@ -76,6 +76,29 @@ enum TraceEv { TR_ENTRY = 0, TR_PRO, TR_LOOP, TR_PUB, TR_GRP, TR_TOP, TR_FIN, TR
         if (TRACE_ON(g_) && threadIdx.x == 0)                                                      \
             (g_).trace[((size_t)(pass_) * TR_MAXWG + blockIdx.x) * TR_SLOTS + (ev_)] = wall_clock64(); \
     } while (0)
+// contiguous trial range [b0, b1) of this workgroup in a streaming pass: a static, call-invariant
+// assignment, so each partial row sums a fixed trial set in a fixed order.  (An uneven split between
+// a CU's first and second resident workgroup was measured and does not move the pass's end: the CU
+// pair's joint throughput does.)
+__device__ __forceinline__ void trial_range(const Geo& g, int& b0, int& b1) {
+    const long long w = blockIdx.x, G = gridDim.x;
+    b0 = (int)(w * g.B / G);
+    b1 = (int)((w + 1) * g.B / G);
+}
+
+// fine stamps of the reduction / finalize critical path (row TR_FINE + pass, slot k), thread 0 only
+constexpr int TR_FINE = 6;
+#define TRACE_FS(g_, pass_, k_)                                                                  \
+    do {                                                                                         \
+        if (TRACE_ON(g_) && threadIdx.x == 0)                                                      \
+            (g_).trace[((size_t)TR_FINE * TR_MAXWG + (pass_)) * TR_SLOTS + (k_)] = wall_clock64(); \
+    } while (0)
+// per-workgroup prologue stamps of one pass (row TR_FINE + 1, slot k)
+#define TRACE_PS(g_, k_)                                                                         \
+    do {                                                                                         \
+        if (TRACE_ON(g_) && threadIdx.x == 0)                                                      \
+            (g_).trace[((size_t)(TR_FINE + 1) * TR_MAXWG + blockIdx.x) * TR_SLOTS + (k_)] = wall_clock64(); \
+    } while (0)
 #define TRACE_PH(g_, pass_, ph_, t0_)                                                            \
     do {                                                                                         \
         if (TRACE_ON(g_) && threadIdx.x == 0) {                                                  \
@@ -116,8 +139,9 @@ enum PassCMode { PC_LOGITS = 1, PC_BWD = 2, PC_CE = 4 };
 // In-kernel reduction + finalize (eegnet_finalize.hip): every pass kernel ends with a ticketed
 // two-level fp64 reduction of its per-workgroup partial rows; the last workgroup to arrive runs that
 // pass's finalize.  Ticket words: NCNT per pass, zeroed by a memset node at the start of every call.
-constexpr int NGRPMAX = 15;
-constexpr int NCNT = 16;          // [0, ngrp) group tickets, [NCNT-1] the top-level ticket
+constexpr int KSMAX = 16;       // ws MFMA k-steps: ceil(C / 4), C <= 64
+constexpr int NGRPMAX = 32;      // groups <= NCNT - 1 (ticket words)
+constexpr int NCNT = 40;          // [0, ngrp) group tickets, [NCNT-1] the top-level ticket
 constexpr int TK_PASSES = 5;      // ticket blocks: passes A..E, contiguous from pass A's
 struct FinArgs {
     double* part2;                // [ngrp][ncols] fp64 group partials
@@ -206,6 +230,32 @@ __device__ __forceinline__ float keep_mul(const Geo& g, const uint8_t* __restric
 // the NEXT trial's x prefetch issued at the top of the iteration.  One explicit drain here resolves
 // those operands for good.
 __device__ __forceinline__ void drain_prologue_loads() { __builtin_amdgcn_s_waitcnt(0); }
+
+// Batched staging of a small global array into LDS: U unconditional loads per thread (indices
+// clamped, so no per-load branch and wait), then the guarded stores.  Callers issue every batch they
+// need before the first store, so a finalize pays one global round trip instead of one per element
+// group.  Elements beyond U * blockDim.x (large non-default geometries) are copied by store() itself.
+template <int U, typename T>
+struct Stage {
+    T v[U];
+    const T* src;
+    __device__ __forceinline__ void load(const T* s, int n) {
+        src = s;
+        const int nth = blockDim.x, last = n > 0 ? n - 1 : 0;
+#pragma unroll
+        for (int j = 0; j < U; ++j) v[j] = s[min((int)threadIdx.x + j * nth, last)];
+    }
+    template <typename D>
+    __device__ __forceinline__ void store(D* dst, int n) const {
+        const int nth = blockDim.x;
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int i = threadIdx.x + j * nth;
+            if (i < n) dst[i] = (D)v[j];
+        }
+        for (int i = threadIdx.x + U * nth; i < n; i += nth) dst[i] = (D)src[i];
+    }
+};
 
 // a wave-uniform zero the compiler cannot see through: added to a weight-row offset it pins that
 // row's scalar loads next to their use (otherwise every row of every table is hoisted into SGPRs and
@@ -410,6 +460,32 @@ __device__ __forceinline__ void spatial_mfma(const float* Xs, const float (&aw)[
                 const int c = 4 * s + lk;
                 const float b = (c < C) ? xcol[4 * s * RS] : 0.f;
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aw[s], b, acc, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = 4 * lk + r;
+            if (o < F2) Ss[o * RS + LP + 16 * n + li] = acc[r];
+        }
+    }
+}
+
+// the same with the ws fragments read from an LDS table [KS][64] (per tile: no registers held
+// across the caller's loop)
+template <int KS, int NW = NWAVE>
+__device__ __forceinline__ void spatial_mfma_l(const float* Xs, const float* awl, float* Ss, int C, int F2,
+                                               int NT16, int RS, int LP, int wave, int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+    const int ks = (C + 3) >> 2;
+    for (int n = wave; n < NT16; n += NW) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* xcol = Xs + lk * RS + LP + 16 * n + li;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            if (s < ks) {
+                const int c = 4 * s + lk;
+                const float b = (c < C) ? xcol[4 * s * RS] : 0.f;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(awl[64 * s + lane], b, acc, 0, 0, 0);
             }
         }
 #pragma unroll

@@ -25,6 +25,16 @@ __device__ __forceinline__ void pub(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Agent-coherent loads of published rows (sc1 loads, AMDGPUUsage GFX942 "load atomic monotonic
+// agent"): the reader needs no L2 invalidate (buffer_inv sc1) after its ticket, which measured at
+// microseconds of stall for the loads that follow it.
+__device__ __forceinline__ float ld_pub(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_pub(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // all threads call; returns (workgroup-uniformly) whether this workgroup took the last of `target`
 // tickets on *w.  `flag` is one LDS word nobody else touches between the two barriers.
 __device__ __forceinline__ bool take_ticket(unsigned* w, unsigned target, int* flag) {
@@ -33,10 +43,6 @@ __device__ __forceinline__ bool take_ticket(unsigned* w, unsigned target, int* f
     if (threadIdx.x == 0) {
         const unsigned prev = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = prev == target - 1u;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
         *flag = last;
     }
     __syncthreads();
@@ -46,60 +52,58 @@ __device__ __forceinline__ bool take_ticket(unsigned* w, unsigned target, int* f
 // LDS carve-up of the tail (doubles, from the start of the pass kernel's dynamic LDS, which is no
 // longer in use once the partial row is written): [flag 2][S rup2(ncols)][scratch]
 __host__ __device__ constexpr int tail_scratch_doubles(int ncols) { return ncols > NTH ? ncols : NTH; }
+constexpr int RGB = 16;           // partial rows per group reducer batch (one round trip)
 __host__ __device__ constexpr int tail_s_doubles(int ncols) { return 2 + ((ncols + 1) & ~1); }
 
 __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const FinArgs& fa, double* dsm) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, nth = blockDim.x;
     int* flag = (int*)dsm;
     double* S = dsm + 2;
-    double* scr = dsm + tail_s_doubles(ncols);
-    // partial rows per group / groups from this launch's own grid (passes use different grids)
+    // partial rows per group / groups from this launch's own grid (passes use different grids):
+    // groups of <= RGB rows, so a group reducer fetches each column's rows in one batch
     const int grid = gridDim.x;
-    const int rgs = max(32, (grid + NGRPMAX - 1) / NGRPMAX), ngrp = (grid + rgs - 1) / rgs;
+    const int rgs = max(RGB, (grid + NGRPMAX - 1) / NGRPMAX), ngrp = (grid + rgs - 1) / rgs;
     const int grp = blockIdx.x / rgs;
-    const int r0 = grp * rgs, r1 = min(grid, r0 + rgs), nr = r1 - r0;
+    const int r0 = grp * rgs, r1 = min(grid, r0 + rgs);
     const int tp = fa.tpass;
     TRACE(g, tp, TR_PUB);
-    if (!take_ticket(fa.cnt + grp, (unsigned)nr, flag)) return false;
-    // group reducer: rows [r0, r1), rs interleaved row subsets per column, then the rs-way sum
-    const int rs = max(1, min(nr, (int)blockDim.x / ncols));
-    for (int idx = tid; idx < rs * ncols; idx += (int)blockDim.x) {
-        const int sub = idx / ncols, c = idx - sub * ncols;
+    if (!take_ticket(fa.cnt + grp, (unsigned)(r1 - r0), flag)) return false;
+    TRACE_FS(g, tp, 0);            // last writer wins: about the last group
+    // group reducer: each thread sums whole columns, RGB row loads in flight, in row order
+    for (int c = tid; c < ncols; c += nth) {
         const float* col = part + c;
         double a = 0.0;
-        int r = r0 + sub;
-        for (; r + 7 * rs < r1; r += 8 * rs) {      // 8 loads in flight, summed in row order
-            float v[8];
+        for (int rb = r0; rb < r1; rb += RGB) {
+            // unconditional loads (clamped rows): a guarded load compiles to a branch and a wait each
+            float v[RGB];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = col[(size_t)(r + j * rs) * ncols];
+            for (int j = 0; j < RGB; ++j) v[j] = ld_pub(col + (size_t)min(rb + j, r1 - 1) * ncols);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) a += (double)v[j];
+            for (int j = 0; j < RGB; ++j) a += rb + j < r1 ? (double)v[j] : 0.0;
         }
-        for (; r < r1; r += rs) a += (double)col[(size_t)r * ncols];
-        scr[idx] = a;
-    }
-    __syncthreads();
-    for (int c = tid; c < ncols; c += (int)blockDim.x) {
-        double a = 0.0;
-        for (int sub = 0; sub < rs; ++sub) a += scr[sub * ncols + c];
         pub(fa.part2 + (size_t)grp * ncols + c, a);
     }
     TRACE(g, tp, TR_GRP);
+    TRACE_FS(g, tp, 1);            // last writer wins: about the last group
     if (!take_ticket(fa.cnt + (NCNT - 1), (unsigned)ngrp, flag)) return false;
-    for (int c = tid; c < ncols; c += (int)blockDim.x) {
+    TRACE_FS(g, tp, 2);
+    for (int c = tid; c < ncols; c += nth) {
         double v[NGRPMAX];
 #pragma unroll
-        for (int q = 0; q < NGRPMAX; ++q) v[q] = q < ngrp ? fa.part2[(size_t)q * ncols + c] : 0.0;
+        for (int q = 0; q < NGRPMAX; ++q) v[q] = ld_pub(fa.part2 + (size_t)min(q, ngrp - 1) * ncols + c);
         double a = 0.0;
 #pragma unroll
-        for (int q = 0; q < NGRPMAX; ++q) if (q < ngrp) a += v[q];
+        for (int q = 0; q < NGRPMAX; ++q) a += q < ngrp ? v[q] : 0.0;
         S[c] = a;
     }
-    // every ticket of this pass has been taken: re-arm them (the per-call memset is the guarantee)
+    TRACE_FS(g, tp, 9);
+    // every ticket of this pass has been taken: re-arm them for the next call
     if (tid < ngrp) __hip_atomic_store(fa.cnt + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) __hip_atomic_store(fa.cnt + (NCNT - 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    TRACE_FS(g, tp, 10);
     __syncthreads();
     TRACE(g, tp, TR_TOP);
+    TRACE_FS(g, tp, 3);
     return true;
 }
 
@@ -113,12 +117,19 @@ __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, doub
     *rv = (float)((1.0 - mom) * (double)*rv + mom * var * n / (n - 1.0));
 }
 
-__host__ __device__ constexpr int fin1_scratch_doubles(int K1, int F1) { return K1 * K1 + K1 + 128 + 3 * F1 * K1; }
-__host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1) { return K1 * K1 + K1 + 128 + F1 * K1; }
+// Finalize scratch (doubles) of fin1 / fin5; both begin with ONE batch of global loads into LDS
+// (a finalize runs on the critical path between two launches: every dependent global round trip
+// there is a few hundred ns with the rest of the GPU idle)
+__host__ __device__ constexpr int fin1_scratch_doubles(int K1, int F1, int F2, int C) {
+    return K1 * K1 + K1 + 128 + 3 * F1 * K1 + (F1 * K1 + 2 * F1 + F2 * C + 2 * F1 + 2 * F2 + 1) / 2 + 2;
+}
+__host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1, int nparam) {
+    return K1 * K1 + K1 + 128 + F1 * K1 + (CF_COUNT * CSTR + nparam + 1) / 2 + 2;
+}
 
 // after pass A: BN1 (model.py:32) and BN2 (model.py:47) batch statistics
 __device__ void fin1(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
-    const int K1 = g.K1, F1 = g.F1;
+    const int K1 = g.K1, F1 = g.F1, F2 = g.F2, C = g.C, nth = blockDim.x;
     double* Gm = scr;                 // K1*K1
     double* S1 = Gm + K1 * K1;        // K1
     double* a1s = S1 + K1;            // F1 (<= 64)
@@ -126,7 +137,24 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     double* wd = c1s + 64;            // F1*K1 temporal taps
     double* pq = wd + F1 * K1;        // F1*K1 w[k] (G w)[k]
     double* pm = pq + F1 * K1;        // F1*K1 w[k] S1[k]
+    // staged global inputs (floats): w1 | g1 | b1 | ws | rm1 rv1 | rm2 rv2
+    float* pl = (float*)(pm + F1 * K1);
+    float* pw1 = pl;
+    float* pg1 = pw1 + F1 * K1;
+    float* pb1 = pg1 + F1;
+    float* pws = pb1 + F1;
+    float* pbn = pws + F2 * C;
     const int tid = threadIdx.x;
+    {   // w1 | g1 | b1 | ws are contiguous in the parameter vector (eegnet_host.hip param layout)
+        const int nl = F1 * K1 + 2 * F1 + F2 * C, nb = 2 * F1 + 2 * F2;
+        Stage<2, float> sp;
+        Stage<1, float> sb;
+        sp.load(prm + g.o_w1, nl);
+        if (fa.update_running) sb.load(fa.bn, nb);
+        sp.store(pl, nl);
+        if (fa.update_running) sb.store(pbn, nb);
+    }
+    TRACE_FS(g, fa.tpass, 11);
     const double* G0 = sums;
     const double S0 = sums[K1];
     const double* H = sums + K1 + 1;                 // head pairs (a <= b < R), a-major
@@ -134,7 +162,7 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     const double* hs = Tl + g.nTl;                   // head sample sums [R]
     const double* ts = hs + g.R;                     // tail sample sums [P]
     const double* Sv = ts + g.P;
-    const double* Sv2 = Sv + g.F2;
+    const double* Sv2 = Sv + F2;
     // lag-Gram of the padded rows: G[k][k+d] = G0[d] + sum_{j<k} Ed[d][j], with
     // Ed[d][j] = sum_c X[T+j]X[T+j+d] - X[j]X[j+d] = Tl[j][j+d] (j+d < P) - H[j-P][j-P+d] (j >= P)
     if (tid < K1) {
@@ -162,11 +190,14 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
             if (k < K1 - 1) acc += (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
         }
     }
-    for (int i = tid; i < F1 * K1; i += (int)blockDim.x) wd[i] = (double)prm[g.o_w1 + i];
     __syncthreads();
-    for (int i = tid; i < K1 * K1 + K1; i += (int)blockDim.x) fa.stats[i] = Gm[i];
+    TRACE_FS(g, fa.tpass, 4);
+    for (int i = tid; i < F1 * K1; i += nth) wd[i] = (double)pw1[i];
+    for (int i = tid; i < K1 * K1 + K1; i += nth) fa.stats[i] = Gm[i];
+    __syncthreads();
+    TRACE_FS(g, fa.tpass, 5);
     // quadratic forms w^T G w and w^T S1, one (filter, tap) per thread (G symmetric: column reads)
-    for (int p = tid; p < F1 * K1; p += (int)blockDim.x) {
+    for (int p = tid; p < F1 * K1; p += nth) {
         const int gg = p / K1, k = p - gg * K1;
         const double* w = wd + gg * K1;
         double r = 0.0;
@@ -175,28 +206,34 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
         pm[p] = w[k] * S1[k];
     }
     __syncthreads();
-    const double n1 = (double)g.B * g.C * g.T;
+    TRACE_FS(g, fa.tpass, 6);
+    const double n1 = (double)g.B * C * g.T;
     if (tid < F1) {
         double mu = 0.0, e2 = 0.0;
         for (int k = 0; k < K1; ++k) { mu += pm[tid * K1 + k]; e2 += pq[tid * K1 + k]; }
         mu /= n1;
         const double var = e2 / n1 - mu * mu;
         const double inv = 1.0 / sqrt(var + (double)g.eps);
-        const double a1 = (double)prm[g.o_g1 + tid] * inv;
-        const double c1 = (double)prm[g.o_b1 + tid] - a1 * mu;
+        const double a1 = (double)pg1[tid] * inv;
+        const double c1 = (double)pb1[tid] - a1 * mu;
         a1s[tid] = a1; c1s[tid] = c1;
         fa.coef[CF_A1 * CSTR + tid] = (float)a1;
         fa.coef[CF_C1 * CSTR + tid] = (float)c1;
         fa.coef[CF_INV1 * CSTR + tid] = (float)inv;
         fa.coef[CF_MU1 * CSTR + tid] = (float)mu;
-        if (fa.update_running) bn_running(fa.bn + tid, fa.bn + F1 + tid, mu, var, n1, g.mom);
+        if (fa.update_running) {
+            const double mom = g.mom;
+            fa.bn[tid] = (float)((1.0 - mom) * (double)pbn[tid] + mom * mu);
+            fa.bn[F1 + tid] = (float)((1.0 - mom) * (double)pbn[F1 + tid] + mom * var * n1 / (n1 - 1.0));
+        }
     }
     __syncthreads();
+    TRACE_FS(g, fa.tpass, 7);
     const double n2 = (double)g.B * g.T;
-    if (tid < g.F2) {
+    if (tid < F2) {
         const int o = tid, gg = o / g.D;
         double W = 0.0;
-        for (int c = 0; c < g.C; ++c) W += (double)prm[g.o_ws + o * g.C + c];
+        for (int c = 0; c < C; ++c) W += (double)pws[o * C + c];
         const double mv = Sv[o] / n2;
         const double varv = Sv2[o] / n2 - mv * mv;
         const double mu2 = a1s[gg] * mv + c1s[gg] * W;
@@ -207,8 +244,12 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
         fa.coef[CF_BE2 * CSTR + o] = (float)(-alpha * mv);
         fa.coef[CF_INV2 * CSTR + o] = (float)inv2;
         fa.coef[CF_W * CSTR + o] = (float)W;
-        float* rm2 = fa.bn + 2 * F1;
-        if (fa.update_running) bn_running(rm2 + o, rm2 + g.F2 + o, mu2, var2, n2, g.mom);
+        if (fa.update_running) {
+            const double mom = g.mom;
+            float* rm2 = fa.bn + 2 * F1;
+            rm2[o] = (float)((1.0 - mom) * (double)pbn[2 * F1 + o] + mom * mu2);
+            rm2[F2 + o] = (float)((1.0 - mom) * (double)pbn[2 * F1 + F2 + o] + mom * var2 * n2 / (n2 - 1.0));
+        }
     }
 }
 
@@ -285,61 +326,100 @@ __device__ __forceinline__ void adam_elem(float* p, float g, float* m, float* v,
 }
 
 // after pass E: spatial grad (+ clamp, model.py:44), BN1 grads, temporal-conv grad; then Adam
+constexpr int APT = 8;            // Adam elements per finalize thread: nparam <= APT * blockDim
 __device__ void fin5(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
-    const int tid = threadIdx.x, K1 = g.K1, F1 = g.F1;
-    double* Gm = scr;                 // K1*K1 (+ S1 K1), copied from fa.stats
+    const int tid = threadIdx.x, nth = blockDim.x, K1 = g.K1, F1 = g.F1;
+    double* Gm = scr;                 // K1*K1 (+ S1 K1), from fa.stats
     double* S1 = Gm + K1 * K1;
     double* db1s = S1 + K1;           // 64
     double* dg1s = db1s + 64;         // 64
     double* wd = dg1s + 64;           // F1*K1
+    float* cf = (float*)(wd + F1 * K1);          // coefficient block [CF_COUNT][CSTR]
+    float* gL = cf + CF_COUNT * CSTR;            // [0, o_g2): the gradients this finalize computes
     const double* Q = sums;
     const double* Xm = sums + g.F2 * K1;
     const double* Sdy = Xm + g.F2 * g.C;
     const double* Sdyv = Sdy + g.F2;
-    for (int i = tid; i < K1 * K1 + K1; i += (int)blockDim.x) Gm[i] = fa.stats[i];
-    for (int i = tid; i < F1 * K1; i += (int)blockDim.x) wd[i] = (double)prm[g.o_w1 + i];
-    for (int p = tid; p < g.F2 * g.C; p += (int)blockDim.x) {
+    // ---- one batch of global loads: statistics, taps, coefficients, Adam state ----
+    const bool adam = fa.adam_m != nullptr;
+    float ap[APT], am[APT], av[APT], ag[APT];
+    int step0;
+    {
+        Stage<3, double> s0;
+        Stage<1, float> s1;
+        Stage<3, float> s2;
+        s0.load(fa.stats, K1 * K1 + K1);
+        s1.load(prm + g.o_w1, F1 * K1);
+        s2.load(fa.coef, CF_COUNT * CSTR);
+        if (adam) {   // parameters, moments and the earlier finalizes' gradients (indices >= o_g2)
+            const int last = g.nparam - 1;
+#pragma unroll
+            for (int j = 0; j < APT; ++j) {
+                const int i = min(tid + nth * j, last);
+                ap[j] = fa.params[i]; am[j] = fa.adam_m[i]; av[j] = fa.adam_v[i]; ag[j] = fa.grads[i];
+            }
+        }
+        step0 = adam ? *fa.step : 0;
+        s0.store(Gm, K1 * K1 + K1);
+        s1.store(wd, F1 * K1);
+        s2.store(cf, CF_COUNT * CSTR);
+    }
+    __syncthreads();
+    TRACE_FS(g, fa.tpass, 4);
+    for (int p = tid; p < g.F2 * g.C; p += nth) {
         const int o = p / g.C, gg = o / g.D;
-        const double v = (double)fa.coef[CF_A1 * CSTR + gg] * Xm[p] + (double)fa.coef[CF_C1 * CSTR + gg] * Sdy[o];
-        fa.grads[g.o_ws + p] = g.noclamp ? (float)v : fminf(fmaxf((float)v, -1.0f), 1.0f);
+        const double v = (double)cf[CF_A1 * CSTR + gg] * Xm[p] + (double)cf[CF_C1 * CSTR + gg] * Sdy[o];
+        const float vf = g.noclamp ? (float)v : fminf(fmaxf((float)v, -1.0f), 1.0f);
+        fa.grads[g.o_ws + p] = vf;
+        gL[g.o_ws + p] = vf;
     }
     if (tid < F1) {
         const int gg = tid;
         double db1 = 0.0, dyu = 0.0;
         for (int o = gg * g.D; o < (gg + 1) * g.D; ++o) {
-            db1 += (double)fa.coef[CF_W * CSTR + o] * Sdy[o];
+            db1 += (double)cf[CF_W * CSTR + o] * Sdy[o];
             dyu += Sdyv[o];
         }
-        const double inv1 = fa.coef[CF_INV1 * CSTR + gg], mu1 = fa.coef[CF_MU1 * CSTR + gg];
+        const double inv1 = cf[CF_INV1 * CSTR + gg], mu1 = cf[CF_MU1 * CSTR + gg];
         const double dg1 = inv1 * (dyu - mu1 * db1);
         db1s[gg] = db1; dg1s[gg] = dg1;
         fa.grads[g.o_b1 + gg] = (float)db1;
         fa.grads[g.o_g1 + gg] = (float)dg1;
+        gL[g.o_b1 + gg] = (float)db1;
+        gL[g.o_g1 + gg] = (float)dg1;
     }
     __syncthreads();
+    TRACE_FS(g, fa.tpass, 5);
     const double n1 = (double)g.B * g.C * g.T;
-    for (int p = tid; p < F1 * K1; p += (int)blockDim.x) {
+    for (int p = tid; p < F1 * K1; p += nth) {
         const int gg = p / K1, k = p - gg * K1;
         const double* w = wd + gg * K1;
         double qg = 0.0;
         for (int o = gg * g.D; o < (gg + 1) * g.D; ++o) qg += Q[o * K1 + k];
         double ux = 0.0;
         for (int l = 0; l < K1; ++l) ux += w[l] * Gm[l * K1 + k];
-        const double inv1 = fa.coef[CF_INV1 * CSTR + gg], mu1 = fa.coef[CF_MU1 * CSTR + gg];
+        const double inv1 = cf[CF_INV1 * CSTR + gg], mu1 = cf[CF_MU1 * CSTR + gg];
         const double xhx = inv1 * (ux - mu1 * S1[k]);
-        const double a1 = fa.coef[CF_A1 * CSTR + gg];
+        const double a1 = cf[CF_A1 * CSTR + gg];
         const double v = a1 * (qg - db1s[gg] / n1 * S1[k] - dg1s[gg] / n1 * xhx);
         fa.grads[g.o_w1 + p] = (float)v;
+        gL[g.o_w1 + p] = (float)v;
     }
-    if (!fa.adam_m) return;
-    __syncthreads();                  // this workgroup's gradient stores are visible to all its waves
-    const int s = *fa.step + 1;
+    if (!adam) return;
+    __syncthreads();                  // gL complete
+    TRACE_FS(g, fa.tpass, 6);
+    const int s = step0 + 1;
     const float step_size = (float)((double)fa.lr / (1.0 - pow((double)fa.b1, (double)s)));
     const float bc2s = (float)sqrt(1.0 - pow((double)fa.b2, (double)s));
-    for (int i = tid; i < g.nparam; i += (int)blockDim.x)
-        adam_elem(fa.params + i, fa.grads[i], fa.adam_m + i, fa.adam_v + i, fa.b1, fa.b2, step_size,
-                  bc2s, fa.eps);
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < APT; ++j) {
+        const int i = tid + nth * j;
+        if (i < g.nparam) {
+            const float gr = i < g.o_g2 ? gL[i] : ag[j];
+            adam_elem(&ap[j], gr, &am[j], &av[j], fa.b1, fa.b2, step_size, bc2s, fa.eps);
+            fa.params[i] = ap[j]; fa.adam_m[i] = am[j]; fa.adam_v[i] = av[j];
+        }
+    }
     if (tid == 0) *fa.step = s;
 }
 

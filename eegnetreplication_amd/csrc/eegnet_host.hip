@@ -24,7 +24,7 @@ static inline int rup(int a, int m) { return (a + m - 1) / m * m; }
 static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
 
 enum { TK_A = 0, TK_B, TK_C, TK_D, TK_E, TK_COUNT };
-constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 320 B, a multiple of 16
+constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 800 B, a multiple of 16
 
 struct WsLayout {
     size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, total;
@@ -103,16 +103,16 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nwD = std::max(1, std::min(NTHS / 64, (LDS_MAX / 4) / pwD));
     g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);
     g->ldsD = std::max(g->nwD * pwD, g->nwD * g->nD);
-    g->ldsE = std::max(rows1 + 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4),
+    g->ldsE = std::max(rows1 + 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4) + 8 * g->F2 + 64 * KSMAX,
                        NWB * 256);                                // after the loop: dws tiles
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
     auto tail = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + std::max(tail_scratch_doubles(ncols), fin)); };
-    g->ldsA = std::max(g->ldsA, tail(g->nA, fin1_scratch_doubles(g->K1, g->F1)));
+    g->ldsA = std::max(g->ldsA, tail(g->nA, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C)));
     g->ldsB = std::max(g->ldsB, tail(g->nB, 0));
     g->ldsC = std::max(g->ldsC, tail(g->nC, 0));
     g->ldsD = std::max(g->ldsD, tail(g->nD, 0));
-    g->ldsE = std::max(g->ldsE, tail(g->nE, fin5_scratch_doubles(g->K1, g->F1)));
+    g->ldsE = std::max(g->ldsE, tail(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->nparam)));
     if (launch) {
         if (g->F2 > F2MAX)
             return fail(EEGNET_EINVAL, "F1*D = %d > %d: the row-per-wave train step covers F2 <= %d "
@@ -125,6 +125,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
         if ((double)g->B * g->F2 * g->T1 >= 4294967296.0)
             return fail(EEGNET_EINVAL, "B*F2*(T/4) must stay below 2^32 (dropout / mask indices)");
         if (g->NF > 64 * MAXNFQ) return fail(EEGNET_EINVAL, "F2*(T/32) = %d > %d", g->NF, 64 * MAXNFQ);
+        if (g->nparam > APT * NTB) return fail(EEGNET_EINVAL, "%d parameters > %d", g->nparam, APT * NTB);
         const int lmax = std::max(std::max(std::max(g->ldsA, g->ldsB), std::max(g->ldsC, g->ldsD)),
                                   std::max(g->ldsE, g->ldsI));
         if (lmax * 4 > LDS_MAX) return fail(EEGNET_EINVAL, "dims need %d B of LDS (> %d)", lmax * 4, LDS_MAX);

@@ -42,6 +42,30 @@ __device__ __forceinline__ void x_dma(const float* __restrict__ xb, int C, int T
     }
 }
 
+// Zero the workgroup's LDS rows [0, n) before the first trial.  With LDS-DMA staging (SKIPX) the x
+// data windows [LP, LP + T) of the first C rows are left to the DMA, so fill and DMA touch disjoint
+// words and need no barrier between them (the barrier would also wait for every weight load).
+template <bool SKIPX>
+__device__ __forceinline__ void zero_fill(float* sm, int n, int C, int RS, int LP, int T, int tid) {
+    if constexpr (SKIPX) {
+        const int wave = tid >> 6, lane = tid & 63;
+        for (int r = wave; r < C; r += NWB) {
+            float* row = sm + r * RS;
+            for (int k = lane; k < LP; k += 64) row[k] = 0.f;
+            for (int k = LP + T + lane; k < RS; k += 64) row[k] = 0.f;
+        }
+        for (int i = C * RS + tid; i < n; i += NTB) sm[i] = 0.f;
+    } else {
+        for (int i = tid; i < n; i += NTB) sm[i] = 0.f;
+    }
+}
+
+// LDS-DMA of n floats (n % 256 == 0, 16-byte aligned source) into a contiguous LDS array
+__device__ __forceinline__ void flat_dma(const float* __restrict__ src, int n, float* dst, int wave, int lane) {
+    for (int i = wave; i < (n >> 8); i += NWB)
+        __builtin_amdgcn_global_load_lds((gvoid_t*)(src + 256 * i + 4 * lane), (lvoid_t*)(dst + 256 * i), 16, 0, 0);
+}
+
 // this half-wave's taps (a per-lane select only when the two rows of a wave use different filters)
 template <int K1, int NTS>
 __device__ __forceinline__ void half_taps(const float (&tap)[NTS][K1], int hr, float (&tl)[K1]) {
@@ -92,8 +116,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     float* red = Ss + F2 * RS;                        // NWB * (K1 + 1)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int b0, b1;
+    trial_range(g, b0, b1);
 
-    for (int i = tid; i < (C + F2) * RS; i += NTB) sm[i] = 0.f;
+    zero_fill<TT && (TT % 256 == 0)>(sm, (C + F2) * RS, C, RS, LP, T, tid);
     float aw[KS];
     load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
     float tap[NTS][K1];
@@ -131,11 +157,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     constexpr bool XDMA = TT && (TT % 256 == 0);
     float pf[XDMA ? 1 : PF];
     if constexpr (XDMA) {
-        __syncthreads();                                 // the zero fill precedes the DMA writes
-        if ((int)blockIdx.x < g.B) x_dma(x + (size_t)blockIdx.x * C * T, C, T, RS, LP, Xb, wave, lane);
+        if (b0 < b1) x_dma(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
         __syncthreads();
     } else {
-        if ((int)blockIdx.x < g.B) x_prefetch<PF, NTB>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
+        if (b0 < b1) x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pf, tid);
         __syncthreads();
         x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         __syncthreads();
@@ -144,10 +169,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     TRACE(g, 0, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        const int bn = b + gridDim.x;
+    for (int b = b0; b < b1; ++b) {
+        const int bn = b + 1;
         if constexpr (!XDMA)
-            if (bn < g.B) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
+            if (bn < b1) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
         spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
         // lag-Gram: items (c, quad), lanes of a wave on consecutive quads of one row
         for (int j = tid; j < C * TQ; j += NTB) {
@@ -191,7 +216,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         TRACE_PH(g, 0, 0, tph_);
         __syncthreads();                                   // Ss complete, x read for good
         if constexpr (XDMA)
-            if (bn < g.B) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+            if (bn < b1) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 0, 1, tph_);
         // v = 32-tap FIR of this wave's s rows; BN2 sums of v
         {
@@ -213,7 +238,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         }
         TRACE_PH(g, 0, 2, tph_);
         if constexpr (!XDMA)
-            if (bn < g.B) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+            if (bn < b1) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         TRACE_PH(g, 0, 3, tph_);
         __syncthreads();                                   // Xb staged, Ss free
         TRACE_PH(g, 0, 4, tph_);
@@ -289,8 +314,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     float* Wt = Qs + F2 * RS2;         // block-2 weights, read with wave-uniform addresses
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int b0, b1;
+    trial_range(g, b0, b1);
 
-    for (int i = tid; i < (C + F2) * RS + 2 * F2 * RS2; i += NTB) sm[i] = 0.f;
+    zero_fill<TT && (TT % 256 == 0)>(sm, (C + F2) * RS + 2 * F2 * RS2, C, RS, LP, T, tid);
     for (int i = tid; i < F2MAX * (K2 + F2MAX); i += NTB) {
         float v = 0.f;
         if (i < F2MAX * K2) { if (i < F2 * K2) v = prm[g.o_w2 + i]; }
@@ -318,11 +345,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     constexpr bool XDMA = TT && (TT % 256 == 0);
     float pf[XDMA ? 1 : PF];
     if constexpr (XDMA) {
-        __syncthreads();                                 // the zero fill precedes the DMA writes
-        if ((int)blockIdx.x < g.B) x_dma(x + (size_t)blockIdx.x * C * T, C, T, RS, LP, Xb, wave, lane);
+        if (b0 < b1) x_dma(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
         __syncthreads();
     } else {
-        if ((int)blockIdx.x < g.B) x_prefetch<PF, NTB>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
+        if (b0 < b1) x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pf, tid);
         __syncthreads();
         x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         __syncthreads();
@@ -331,15 +357,15 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     TRACE(g, 1, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        const int bn = b + gridDim.x;
+    for (int b = b0; b < b1; ++b) {
+        const int bn = b + 1;
         if constexpr (!XDMA)
-            if (bn < g.B) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
+            if (bn < b1) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
         spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
         TRACE_PH(g, 1, 0, tph_);
         __syncthreads();                                   // Ss complete; Qs free; x read for good
         if constexpr (XDMA)
-            if (bn < g.B) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+            if (bn < b1) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 1, 1, tph_);
         // d2 / E1 / E2 stay in registers until the next trial's x is staged: a global store issued
         // before that x_store would hold its vmcnt wait (loads and stores drain in order)
@@ -398,7 +424,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         }
         TRACE_PH(g, 1, 2, tph_);
         if constexpr (!XDMA)
-            if (bn < g.B) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
+            if (bn < b1) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         if (oh < F2) {
 #pragma unroll
             for (int m = 0; m < MO; ++m) {
@@ -475,20 +501,30 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     float* red = sm;                             // NWB * 256 dws tiles, reused after the trial loop
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int b0, b1;
+    trial_range(g, b0, b1);
     const int li = lane & 15, lk = lane >> 4;
 
-    for (int i = tid; i < (C + 2 * F2) * RS; i += NTB) sm[i] = 0.f;
-    float aw[KS];
-    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
+    TRACE_PS(g, 0);
+    zero_fill<TT && (TT % 256 == 0)>(sm, (C + 2 * F2) * RS, C, RS, LP, T, tid);
+    TRACE_PS(g, 1);
     float tap[NTS][K1];
     load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
-    // BN2 forward / backward constants of this lane's row (half-wave hr = lane >> 5)
-    float alh, beh, gah, bth, Aoh, Boh, Coh;
-    {
-        const int o = RPW * wave + (lane >> 5), oo = o < F2 ? o : 0;
-        alh = coef[CF_AL2 * CSTR + oo]; beh = coef[CF_BE2 * CSTR + oo];
-        gah = prm[g.o_g2 + oo]; bth = prm[g.o_b2 + oo];
-        Aoh = coef[CF_AO * CSTR + oo]; Boh = coef[CF_BO * CSTR + oo]; Coh = coef[CF_CO * CSTR + oo];
+    TRACE_PS(g, 2);
+    // BN2 forward / backward constants per row, [F2][8] in LDS (read per trial: seven loop-invariant
+    // registers less at the FIR^T, where the GEMM's x operand is already in flight)
+    float* CT = DP + ((F2 * T1 + 3) & ~3);
+    float* AWL = CT + 8 * F2;                    // ws MFMA fragments [KS][64]
+    for (int i = tid; i < 64 * KS; i += NTB) {
+        const int s_ = i >> 6, o = lane & 15, c = 4 * s_ + (lane >> 4);
+        AWL[i] = (o < F2 && c < C) ? prm[g.o_ws + o * C + c] : 0.f;
+    }
+    if (tid < 8 * F2) {
+        const int o = tid >> 3, f = tid & 7;
+        const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
+                         : f == 2 ? prm + g.o_g2 : f == 3 ? prm + g.o_b2 : f == 4 ? coef + CF_AO * CSTR
+                         : f == 5 ? coef + CF_BO * CSTR : coef + CF_CO * CSTR;
+        CT[tid] = src[o];
     }
     const int NO = EEG_NO(TT);
     float sdyl = 0.f, sdyvl = 0.f;                   // this lane's row (half-wave) sums of dy, dy v
@@ -511,22 +547,33 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     constexpr int NDP = (CC && TT) ? (FF * (TT / 4) + NTB - 1) / NTB : 8;   // F2 * T1 <= NDP * NTB
     const int ndp = F2 * T1;
     float pdp[NDP];
+    // specialised shapes: dp2 rows go straight to LDS by DMA (no registers, no exposed load)
+    constexpr bool DPDMA = TT && (TT % 256 == 0) && FF && ((FF * (TT / 4)) % 256 == 0);
     // with LDS-DMA staging the dws GEMM reads its x operand straight from global memory (L2-warm:
     // the same trial's x was just DMA'd), so the x buffer is free right after the spatial GEMM and
     // the next trial's DMA overlaps the whole FIR / FIR^T phase
     constexpr int NKGW = XDMA ? (TT / 16 + NWB / ((CC + 15) / 16) - 1) / (NWB / ((CC + 15) / 16)) : 1;
     floatx4 xg[NKGW];
     if constexpr (XDMA) {
-        __syncthreads();                                 // the zero fill precedes the DMA writes
-        if ((int)blockIdx.x < g.B) {
-            x_dma(x + (size_t)blockIdx.x * C * T, C, T, RS, LP, Xb, wave, lane);
-            for (int i = tid; i < ndp; i += NTB) DP[i] = dp2g[(size_t)blockIdx.x * ndp + i];
+        if (b0 < b1) {
+            x_dma(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
+            TRACE_PS(g, 3);
+            if constexpr (DPDMA) flat_dma(dp2g + (size_t)b0 * ndp, ndp, DP, wave, lane);
+            else {
+#pragma unroll
+            for (int j = 0; j < NDP; ++j) pdp[j] = dp2g[(size_t)b0 * ndp + min(tid + NTB * j, ndp - 1)];
+#pragma unroll
+            for (int j = 0; j < NDP; ++j)
+                if (tid + NTB * j < ndp) DP[tid + NTB * j] = pdp[j];
+            for (int i = tid + NTB * NDP; i < ndp; i += NTB) DP[i] = dp2g[(size_t)b0 * ndp + i];
+            }
+            TRACE_PS(g, 4);
         }
         __syncthreads();
     } else {
-        if ((int)blockIdx.x < g.B) {
-            x_prefetch<PF, NTB>(x + (size_t)blockIdx.x * C * T, C, T, pf, tid);
-            for (int i = tid; i < ndp; i += NTB) DP[i] = dp2g[(size_t)blockIdx.x * ndp + i];
+        if (b0 < b1) {
+            x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pf, tid);
+            for (int i = tid; i < ndp; i += NTB) DP[i] = dp2g[(size_t)b0 * ndp + i];
         }
         __syncthreads();
         x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
@@ -536,13 +583,13 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     TRACE(g, 4, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
-    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        const int bn = b + gridDim.x;
-        spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+    for (int b = b0; b < b1; ++b) {
+        const int bn = b + 1;
+        spatial_mfma_l<KS, NWB>(Xb, AWL, Ss, C, F2, NT16, RS, LP, wave, lane);
         TRACE_PH(g, 4, 0, tph_);
         __syncthreads();                                   // Ss, DP complete
         if constexpr (XDMA)
-            if (bn < g.B) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+            if (bn < b1) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 1, tph_);
         {
             const int hr = lane >> 5, oh = RPW * wave + hr;
@@ -551,6 +598,9 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             if (oh < F2) {
                 const float* row = Ss + oh * RS;
                 float* drow = Dys + oh * RS + LP;
+                const floatx4 c0 = lds_ld4(CT + 8 * oh), c1 = lds_ld4(CT + 8 * oh + 4);
+                const float alh = c0[0], beh = c0[1], gah = c0[2], bth = c0[3];
+                const float Aoh = c1[0], Boh = c1[1], Coh = c1[2];
                 for (int oc = lane & 31; oc < NO; oc += 32) {
                     float w[4 * G_::NW8];
                     lds_window<G_::NW8>(row + 8 * oc, w);
@@ -581,6 +631,22 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 }
             }
             wave_lds_fence();                              // dy rows complete; s rows consumed
+            // this trial's x operand of the dws GEMM, issued here so the FIR^T covers its latency
+            // (the FIR^T holds fewer live registers than the forward FIR + lag correlation)
+        if constexpr (XDMA) {
+            const int c = ct * 16 + li;
+            const float* xr = x + ((size_t)b * C + (c < C ? c : 0)) * T + 4 * lk;
+#pragma unroll
+            for (int j = 0; j < NKGW; ++j) {
+                const int kg = kg0 + j;
+#ifdef EXP_NOXG
+                const floatx4 v = (floatx4){0.f, 0.f, 0.f, 0.f};
+#else
+                const floatx4 v = *reinterpret_cast<const floatx4*>(xr + 16 * min(kg, NT16 - 1));
+#endif
+                xg[j] = (gemm_on && kg < kg1 && c < C) ? v : (floatx4){0.f, 0.f, 0.f, 0.f};
+            }
+        }
             // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
             if (oh < F2) {
                 const float* dyr = Dys + oh * RS;
@@ -606,25 +672,30 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         // the next trial's dp2 is fetched here, its x after the GEMM: their registers must not be
         // live across the FIR / FIR^T phase (the kernel's register peak, 128 VGPRs at 4 waves/SIMD);
         // the other workgroup on the CU covers the exposed latency
-        if (bn < g.B) {
+        // (unconditional loads at clamped addresses: a guarded load compiles to a branch and a wait)
+        if (!DPDMA && bn < b1) {
 #pragma unroll
-            for (int j = 0; j < NDP; ++j) {
-                const int i = tid + NTB * j;
-                if (i < ndp) pdp[j] = dp2g[(size_t)bn * ndp + i];
-            }
+            for (int j = 0; j < NDP; ++j) pdp[j] = dp2g[(size_t)bn * ndp + min(tid + NTB * j, ndp - 1)];
         }
-        if constexpr (XDMA) {                              // this trial's x operand of the dws GEMM
+        if constexpr (XDMA) {
             const int c = ct * 16 + li;
             const float* xr = x + ((size_t)b * C + (c < C ? c : 0)) * T + 4 * lk;
 #pragma unroll
-            for (int j = 0; j < NKGW; ++j) {
+            for (int j = NKGW; j < NKGW; ++j) {
                 const int kg = kg0 + j;
-                xg[j] = (gemm_on && kg < kg1 && c < C) ? *reinterpret_cast<const floatx4*>(xr + 16 * kg)
-                                                      : (floatx4){0.f, 0.f, 0.f, 0.f};
+#ifdef EXP_NOXG
+                const floatx4 v = (floatx4){0.f, 0.f, 0.f, 0.f};
+#else
+                const floatx4 v = *reinterpret_cast<const floatx4*>(xr + 16 * min(kg, NT16 - 1));
+#endif
+                xg[j] = (gemm_on && kg < kg1 && c < C) ? v : (floatx4){0.f, 0.f, 0.f, 0.f};
             }
         }
+        TRACE_PH(g, 4, 6, tph_);
         __syncthreads();                                   // e rows complete
         TRACE_PH(g, 4, 3, tph_);
+        if constexpr (DPDMA)                               // every DP reader is past: next trial's dp2
+            if (bn < b1) flat_dma(dp2g + (size_t)bn * ndp, ndp, DP, wave, lane);
         // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
         // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
         if (gemm_on) {
@@ -659,7 +730,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 }
             }
         }
-        if (bn < g.B) {                            // next trial's dp2 rows: every FIR reader is past
+        if (!DPDMA && bn < b1) {                  // next trial's dp2 rows: every FIR reader is past
 #pragma unroll
             for (int j = 0; j < NDP; ++j) {
                 const int i = tid + NTB * j;
@@ -671,7 +742,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         __syncthreads();                                   // x and e rows consumed
         TRACE_PH(g, 4, 5, tph_);
         if constexpr (!XDMA) {
-            if (bn < g.B) {
+            if (bn < b1) {
                 x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
                 TRACE_PH(g, 4, 6, tph_);
                 __syncthreads();                           // next trial's x staged

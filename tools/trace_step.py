@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--C", type=int, default=22)
     ap.add_argument("--T", type=int, default=256)
+    ap.add_argument("--dump", default=None, help="save the raw stamp array (.npy)")
     args = ap.parse_args()
     from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
     lib = _lib.load()
@@ -46,6 +47,8 @@ def main():
     torch.cuda.synchronize()
     lib.eegnet_trace_enable(None)
     a = buf.cpu().numpy().reshape(8, MAXWG, SLOTS).astype(np.float64)
+    if args.dump:
+        np.save(args.dump, a)
     grids = [int((a[p, :, 0] > 0).sum()) for p in range(5)]
     grid = grids[0]
     t0 = a[0, :grid, 0].min()
@@ -75,6 +78,17 @@ def main():
             line += f" | gap {(ent.min()-prev_end)/100:5.1f}"
         prev_end = end
         print(line)
+        fs = a[6, p]
+        if fs[3] > 0:
+            ks = [k for k in range(16) if fs[k] > 0]
+            print("    reduce/finalize stamps (µs after last publish):",
+                  " ".join(f"{k}:{(fs[k]-pub.max())/100:.2f}" for k in ks))
+        if p == 4:
+            ps = a[7, :grids[p], :8]
+            ks = [k for k in range(8) if (ps[:, k] > 0).any()]
+            if ks:
+                print("    prologue stamps (µs after entry, mean over workgroups):",
+                      " ".join(f"{k}:{np.mean(ps[:, k]-ent)/100:.2f}" for k in ks), f"pro:{np.mean(pro-ent)/100:.2f}")
         ph = st[:, 8:16].mean(axis=0) / ntr
         if ph.any():
             print("    in-loop phases (shader cycles per trial, wave 0):", " ".join(f"{v:.0f}" for v in ph))
