@@ -121,7 +121,7 @@ __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, doub
 // (a finalize runs on the critical path between two launches: every dependent global round trip
 // there is a few hundred ns with the rest of the GPU idle)
 __host__ __device__ constexpr int fin1_scratch_doubles(int K1, int F1, int F2, int C) {
-    return K1 * K1 + K1 + 128 + 3 * F1 * K1 + (F1 * K1 + 2 * F1 + F2 * C + 2 * F1 + 2 * F2 + 1) / 2 + 2;
+    return K1 * K1 + K1 + 128 + (F1 * K1 + 2 * F1 + F2 * C + 2 * F1 + 2 * F2 + 1) / 2 + 2;
 }
 __host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1, int nparam) {
     return K1 * K1 + K1 + 128 + F1 * K1 + (CF_COUNT * CSTR + nparam + 1) / 2 + 2;
@@ -134,11 +134,8 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     double* S1 = Gm + K1 * K1;        // K1
     double* a1s = S1 + K1;            // F1 (<= 64)
     double* c1s = a1s + 64;
-    double* wd = c1s + 64;            // F1*K1 temporal taps
-    double* pq = wd + F1 * K1;        // F1*K1 w[k] (G w)[k]
-    double* pm = pq + F1 * K1;        // F1*K1 w[k] S1[k]
     // staged global inputs (floats): w1 | g1 | b1 | ws | rm1 rv1 | rm2 rv2
-    float* pl = (float*)(pm + F1 * K1);
+    float* pl = (float*)(c1s + 64);
     float* pw1 = pl;
     float* pg1 = pw1 + F1 * K1;
     float* pb1 = pg1 + F1;
@@ -164,71 +161,79 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     const double* Sv = ts + g.P;
     const double* Sv2 = Sv + F2;
     // lag-Gram of the padded rows: G[k][k+d] = G0[d] + sum_{j<k} Ed[d][j], with
-    // Ed[d][j] = sum_c X[T+j]X[T+j+d] - X[j]X[j+d] = Tl[j][j+d] (j+d < P) - H[j-P][j-P+d] (j >= P)
-    if (tid < K1) {
-        const int d = tid;
-        double acc = G0[d];
-        for (int k = 0; k + d < K1; ++k) {
-            Gm[k * K1 + k + d] = acc;
-            Gm[(k + d) * K1 + k] = acc;
-            if (k < K1 - 1 - d) {
-                const int j = k;
-                double ed = 0.0;
-                if (j + d < g.P) ed += Tl[j * g.P - j * (j - 1) / 2 + d];
-                if (j >= g.P) {
-                    const int a = j - g.P;
-                    ed -= H[a * g.R - a * (a - 1) / 2 + d];
-                }
-                acc += ed;
+    // Ed[d][j] = sum_c X[T+j]X[T+j+d] - X[j]X[j+d] = Tl[j][j+d] (j+d < P) - H[j-P][j-P+d] (j >= P).
+    // One K1-lane segment per lag d (K1 | 64: segments never straddle a wave), prefix sums by
+    // shuffle scan: no serial chain over k.
+    for (int t = tid; t < K1 * K1; t += nth) {
+        const int d = t / K1, j = t - d * K1;
+        double e = 0.0;
+        if (j < K1 - 1 - d) {
+            if (j + d < g.P) e += Tl[j * g.P - j * (j - 1) / 2 + d];
+            if (j >= g.P) {
+                const int a = j - g.P;
+                e -= H[a * g.R - a * (a - 1) / 2 + d];
             }
         }
-    }
-    if (tid == 64) {      // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j])
-        double acc = S0;
-        for (int k = 0; k < K1; ++k) {
-            S1[k] = acc;
-            if (k < K1 - 1) acc += (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
+        for (int o = 1; o < K1; o <<= 1) {
+            const double y = __shfl_up(e, o, K1);
+            if (j >= o) e += y;
         }
+        const double base = G0[d];
+        if (j == 0) { Gm[d] = base; Gm[d * K1] = base; }            // k = 0
+        const int k = j + 1;                                        // inclusive(j) = sum_{j' < k}
+        if (k + d < K1) {
+            const double v = base + e;
+            Gm[k * K1 + k + d] = v;
+            Gm[(k + d) * K1 + k] = v;
+        }
+    }
+    if (tid < 64) {       // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j]), same scan
+        const int k = tid;
+        double e = k < K1 - 1 ? (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0) : 0.0;
+        const double own = e;
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_up(e, o, 64);
+            if (k >= o) e += y;
+        }
+        if (k < K1) S1[k] = S0 + (e - own);
     }
     __syncthreads();
     TRACE_FS(g, fa.tpass, 4);
-    for (int i = tid; i < F1 * K1; i += nth) wd[i] = (double)pw1[i];
     for (int i = tid; i < K1 * K1 + K1; i += nth) fa.stats[i] = Gm[i];
-    __syncthreads();
-    TRACE_FS(g, fa.tpass, 5);
-    // quadratic forms w^T G w and w^T S1, one (filter, tap) per thread (G symmetric: column reads)
+    // BN1 moments from the quadratic forms w^T G w and w^T S1: one (filter, tap) per lane, the
+    // filter's K1 lanes reduced by shuffles (G symmetric: column reads)
+    const double n1 = (double)g.B * C * g.T;
     for (int p = tid; p < F1 * K1; p += nth) {
         const int gg = p / K1, k = p - gg * K1;
-        const double* w = wd + gg * K1;
+        const float* w = pw1 + gg * K1;
         double r = 0.0;
-        for (int l = 0; l < K1; ++l) r += Gm[l * K1 + k] * w[l];
-        pq[p] = w[k] * r;
-        pm[p] = w[k] * S1[k];
-    }
-    __syncthreads();
-    TRACE_FS(g, fa.tpass, 6);
-    const double n1 = (double)g.B * C * g.T;
-    if (tid < F1) {
-        double mu = 0.0, e2 = 0.0;
-        for (int k = 0; k < K1; ++k) { mu += pm[tid * K1 + k]; e2 += pq[tid * K1 + k]; }
-        mu /= n1;
-        const double var = e2 / n1 - mu * mu;
-        const double inv = 1.0 / sqrt(var + (double)g.eps);
-        const double a1 = (double)pg1[tid] * inv;
-        const double c1 = (double)pb1[tid] - a1 * mu;
-        a1s[tid] = a1; c1s[tid] = c1;
-        fa.coef[CF_A1 * CSTR + tid] = (float)a1;
-        fa.coef[CF_C1 * CSTR + tid] = (float)c1;
-        fa.coef[CF_INV1 * CSTR + tid] = (float)inv;
-        fa.coef[CF_MU1 * CSTR + tid] = (float)mu;
-        if (fa.update_running) {
-            const double mom = g.mom;
-            fa.bn[tid] = (float)((1.0 - mom) * (double)pbn[tid] + mom * mu);
-            fa.bn[F1 + tid] = (float)((1.0 - mom) * (double)pbn[F1 + tid] + mom * var * n1 / (n1 - 1.0));
+        for (int l = 0; l < K1; ++l) r += Gm[l * K1 + k] * (double)w[l];
+        const double wk = (double)w[k];
+        double q = wk * r, m = wk * S1[k];
+        for (int o = K1 / 2; o > 0; o >>= 1) {
+            q += __shfl_xor(q, o, K1);
+            m += __shfl_xor(m, o, K1);
+        }
+        if (k == 0) {
+            const double mu = m / n1;
+            const double var = q / n1 - mu * mu;
+            const double inv = 1.0 / sqrt(var + (double)g.eps);
+            const double a1 = (double)pg1[gg] * inv;
+            const double c1 = (double)pb1[gg] - a1 * mu;
+            a1s[gg] = a1; c1s[gg] = c1;
+            fa.coef[CF_A1 * CSTR + gg] = (float)a1;
+            fa.coef[CF_C1 * CSTR + gg] = (float)c1;
+            fa.coef[CF_INV1 * CSTR + gg] = (float)inv;
+            fa.coef[CF_MU1 * CSTR + gg] = (float)mu;
+            if (fa.update_running) {
+                const double mom = g.mom;
+                fa.bn[gg] = (float)((1.0 - mom) * (double)pbn[gg] + mom * mu);
+                fa.bn[F1 + gg] = (float)((1.0 - mom) * (double)pbn[F1 + gg] + mom * var * n1 / (n1 - 1.0));
+            }
         }
     }
     __syncthreads();
-    TRACE_FS(g, fa.tpass, 7);
+    TRACE_FS(g, fa.tpass, 5);
     const double n2 = (double)g.B * g.T;
     if (tid < F2) {
         const int o = tid, gg = o / g.D;
