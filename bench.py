@@ -84,6 +84,53 @@ def cpu_baseline(B, C, T, steps, threads):
     return B * steps / dt, dt
 
 
+INFER_BF16_BYTES = lambda C, T: 2 * C * T + 16          # bf16 x in, fp32 logits out, per trial
+# BN-folded inference FLOPs per trial: spatial GEMM + FIR + dw16 + pw + classifier
+INFER_FLOP = lambda C, T, F2, K1=32: 2 * (F2 * C * T + F2 * T * K1 + F2 * (T // 4) * 16
+                                          + F2 * F2 * (T // 4) + 4 * F2 * (T // 32))
+
+
+def bench_infer_bf16(dev, B, C, T, F1, D, steps, warmup):
+    """BASELINE cfg5 inference leg: bf16 batched eval forward of EEGNet-F1,D (random init, running
+    statistics perturbed so BN is not the identity) on synthetic x ~ N(0,1) already in HBM."""
+    from eegnetreplication_amd import EEGNet, _lib
+    torch.manual_seed(1)
+    m = EEGNet(C, T, F1=F1, D=D, p=0.5).to(dev).eval()
+    with torch.no_grad():
+        for name, b in m.named_buffers():
+            if name.endswith("running_var"):
+                b.uniform_(0.5, 1.5)
+    x = torch.randn(B, C, T, device=dev, generator=torch.Generator(device=dev).manual_seed(2)).to(torch.bfloat16)
+    with torch.no_grad():
+        for _ in range(warmup):
+            m(x)
+        _lib.profile_enable(True)
+        m(x)
+        torch.cuda.synchronize()
+        _lib.profile_collect()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = m(x)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        kern = _lib.profile_collect()
+        _lib.profile_enable(False)
+    cnt, tot = kern.get("k_infer_bf16", (0, 0.0))
+    avg_s = tot / max(cnt, 1) * 1e-3
+    by, fl = INFER_BF16_BYTES(C, T), INFER_FLOP(C, T, F1 * D)
+    ach = by * B / avg_s / 1e9
+    return {
+        "metric": f"bf16 batched inference trials/sec EEGNet-{F1},{D} {C}ch x {T}",
+        "value": round(B * steps / dt, 1), "unit": "trials/s", "batch": B, "steps": steps,
+        "dtype": "bf16 operands, fp32 accumulation", "finite": bool(torch.isfinite(out).all()),
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None, "kernel": "k_infer_bf16",
+                     "avg_us": round(avg_s * 1e6, 2), "alg_bytes_per_launch": by * B,
+                     "alg_tflops": round(fl * B / avg_s / 1e12, 2)},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,6 +142,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-infer", action="store_true", help="skip the cfg5 bf16 inference leg")
+    ap.add_argument("--infer-batch", type=int, default=16384)
     args = ap.parse_args()
 
     from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
@@ -188,6 +237,9 @@ def main():
                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic,
                         "kernel": dom, "avg_us": round(avg_s * 1e6, 2),
                         "alg_bytes_per_launch": by * B}
+        infer = None
+        if not args.no_infer:
+            infer = bench_infer_bf16(dev, args.infer_batch, 64, 512, 16, 4, steps=20, warmup=3)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             threads = min(16, len(os.sched_getaffinity(0)))
@@ -219,6 +271,7 @@ def main():
             "ref_formulation_tflops": round(REF_FLOP_PER_TRIAL * trials_per_s / 1e12, 2),
             "kernels": per_kernel,
             "final_loss": round(loss, 5),
+            "cfg5_infer_bf16": infer,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

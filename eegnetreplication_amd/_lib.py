@@ -38,6 +38,7 @@ _SIGS = {
                                        ctypes.c_int]),
     "eegnet_clamp_grads": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp]),
     "eegnet_forward_eval": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp]),
+    "eegnet_forward_eval_bf16": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _vp]),
     "eegnet_adam_step": (ctypes.c_int, [ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_float,
                                         ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp]),
     "eegnet_train_step": (ctypes.c_int, [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, ctypes.c_uint64,

@@ -170,9 +170,9 @@ static void set_key(Geo* g, uint64_t seed, uint64_t offset) {
 }
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
-enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_COUNT };
+enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_INFER_BF16, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
-                                              "k_adam", "k_infer", "memset_tickets"};
+                                              "k_adam", "k_infer", "memset_tickets", "k_infer_bf16"};
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { bool on = false; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
@@ -215,6 +215,9 @@ static void set_attrs_shape() {
 
 static void ensure_attrs() {
     if (g_attr_done) return;
+    for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
+                          (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 0, 0, 0>();
     set_attrs_shape<64, 0, 0, 0>();
     set_attrs_shape<32, 22, 256, 16>();
@@ -295,6 +298,56 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe)
     { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
     } LAUNCH_CHECK("k_pass_e");
+    return 0;
+}
+
+// geometry of the bf16 eval kernel (eegnet_infer_bf16.hip)
+static float* g_bf16_dbg = nullptr;     // eegnet_debug_bf16 (debug builds only)
+
+static int make_geo_bf16(const eegnet_dims* d, GeoI* g) {
+    Geo q;
+    if (int r = make_geo(d, &q, false)) return r;
+    memset(g, 0, sizeof(*g));
+    g->B = q.B; g->C = q.C; g->T = q.T; g->F1 = q.F1; g->D = q.D; g->F2 = q.F2; g->K1 = q.K1; g->P = q.P;
+    g->eps = q.eps;
+    g->o_w1 = q.o_w1; g->o_g1 = q.o_g1; g->o_b1 = q.o_b1; g->o_ws = q.o_ws; g->o_g2 = q.o_g2;
+    g->o_b2 = q.o_b2; g->o_w2 = q.o_w2; g->o_W3 = q.o_W3; g->o_g3 = q.o_g3; g->o_b3 = q.o_b3;
+    g->o_Wfc = q.o_Wfc; g->o_bfc = q.o_bfc;
+    g->CP = rup(g->C, 32); g->KC = g->CP / 32;
+    g->F2P = g->F2 <= 16 ? 16 : g->F2 <= 32 ? 32 : 64;
+    g->NOT = g->F2P / 16;
+    g->F2K = std::max(32, g->F2P); g->KCW = g->F2K / 32;
+    g->TX = rup(g->T, 128);
+    g->NT = (g->T + 15) / 16; g->NBLK = (g->NT + 15) / 16;
+    g->LPs = g->P + 1;
+    g->KSF = (g->K1 + 16 + 31) / 32;
+    g->SXs = rup(256 * g->NBLK + 32 * g->KSF, 64) + 8;
+    g->T1 = g->T / 4; g->T2 = g->T1 / 8; g->NF = g->F2 * g->T2;
+    const int nq = (g->T1 + 3) / 4;
+    g->RA = 4 * nq + 16;
+    g->NT1 = (8 * g->T2 + 15) / 16;
+    g->TZ = rup(std::max(4 * nq, 16 * g->NT1), 128);
+    if (g->T % 8 == 0) {
+        const int units = g->CP * g->TX / 8;
+        int u = (units + NTI - 1) / NTI, p = 1;
+        while (p < u) p *= 2;
+        g->PFU = p;
+    } else {
+        g->PFU = 0;
+    }
+    if (g->PFU > 16) return fail(EEGNET_EINVAL, "bf16 eval: C*T too large for one trial in registers");
+    const int r1 = std::max(g->CP * g->TX * 2, rup(g->F2P * g->RA * 4, 16) + g->F2K * g->TZ * 2);
+    g->offZ = rup(g->F2P * g->RA * 4, 16);
+    g->offS = rup(r1, 16);
+    g->offW1 = rup(g->offS + g->F2P * g->SXs * 2, 16);
+    g->offW2 = rup(g->offW1 + g->F1 * g->K1 * 4, 16);
+    g->offCo = rup(g->offW2 + g->F2P * K2 * 4, 16);
+    g->offL = rup(g->offCo + 4 * g->F2P * 4, 16);
+    g->lds = g->offL + NWI * NCLS * 4;
+    g->dbg = g_bf16_dbg;
+    if (g->lds > LDS_MAX)
+        return fail(EEGNET_EINVAL, "bf16 eval: dims need %d B of LDS (> %d): C=%d T=%d F2=%d", g->lds, LDS_MAX,
+                    g->C, g->T, g->F2);
     return 0;
 }
 
@@ -389,6 +442,30 @@ int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const floa
     return 0;
 }
 
+int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const float* bn_buffers,
+                             const uint16_t* x, float* logits, void* stream) {
+    GeoI g;
+    if (int r = make_geo_bf16(dims, &g)) return r;
+    if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
+    if (int r = check_ptrs(x, "x", logits, "logits")) return r;
+    if (g.PFU > 0 && ((uintptr_t)x & 15))
+        return fail(EEGNET_EINVAL, "bf16 eval: x must be 16-byte aligned");
+    ensure_attrs();
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(std::min(g.B, device_cus())), blk(NTI);
+    PROF(KID_INFER_BF16);
+    switch (g.PFU) {
+        case 0: hipLaunchKernelGGL(k_infer_bf16<0>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
+        case 1: hipLaunchKernelGGL(k_infer_bf16<1>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
+        case 2: hipLaunchKernelGGL(k_infer_bf16<2>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
+        case 4: hipLaunchKernelGGL(k_infer_bf16<4>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
+        case 8: hipLaunchKernelGGL(k_infer_bf16<8>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
+        default: hipLaunchKernelGGL(k_infer_bf16<16>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
+    }
+    LAUNCH_CHECK("k_infer_bf16");
+    return 0;
+}
+
 int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_avg,
                      float* exp_avg_sq, int32_t* step, float lr, float beta1, float beta2,
                      float eps, void* stream) {
@@ -447,6 +524,15 @@ int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream) {
     LAUNCH_CHECK("k_clamp");
     return 0;
 }
+
+#ifdef EEGNET_TRACE
+// debug hook of the traced build: workgroup 0 dumps its first trial's s [F2P,T], a [F2P,T/4] and
+// z [F2P,T/4] planes (fp32) into `buf` (NULL turns it off)
+int eegnet_debug_bf16(float* buf) {
+    g_bf16_dbg = buf;
+    return 0;
+}
+#endif
 
 const char* eegnet_last_error(void) { return g_err.c_str(); }
 

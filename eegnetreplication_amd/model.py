@@ -167,9 +167,15 @@ class EEGNet(nn.Module):
     # -- forward -------------------------------------------------------------------------------
     def forward(self, x):
         require_device(x, "EEGNet input")
+        if x.dtype == torch.bfloat16 and not self.training:
+            # bf16 batched inference: bf16 MFMA operands, fp32 accumulation
+            if x.dim() != 3 or x.shape[1] != self.C or x.shape[2] != self.T:
+                raise RuntimeError(f"expected input [B,{self.C},{self.T}], got {list(x.shape)}")
+            with torch.no_grad():
+                return ops.forward_eval_bf16(self.shape, self.flat_parameters(), self._bn_flat, x)
         if x.dtype != torch.float32:
-            raise RuntimeError(f"EEGNet expects float32 input (got {x.dtype}); the reference "
-                               f"casts with signals.float() (model.py:137)")
+            raise RuntimeError(f"EEGNet expects float32 input (got {x.dtype}; bfloat16 is accepted in "
+                               f"eval mode); the reference casts with signals.float() (model.py:137)")
         if x.dim() != 3 or x.shape[1] != self.C or x.shape[2] != self.T:
             raise RuntimeError(f"expected input [B,{self.C},{self.T}], got {list(x.shape)}")
         if x.requires_grad:

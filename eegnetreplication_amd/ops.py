@@ -141,6 +141,20 @@ def forward_eval(shape: Shape, flat_params, bn_flat, x) -> torch.Tensor:
     return logits
 
 
+def forward_eval_bf16(shape: Shape, flat_params, bn_flat, x) -> torch.Tensor:
+    """Eval-mode forward on bf16 input (bf16 MFMA operands, fp32 accumulation, fp32 logits)."""
+    if x.dtype != torch.bfloat16:
+        raise RuntimeError(f"forward_eval_bf16 expects bfloat16 input (got {x.dtype})")
+    x = x.contiguous()
+    B = x.shape[0]
+    logits = torch.empty((B, NCLS), dtype=torch.float32, device=x.device)
+    d = shape.dims(B)
+    _lib.check(_lib.load().eegnet_forward_eval_bf16(
+        ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(logits), _stream()),
+        "eegnet_forward_eval_bf16")
+    return logits
+
+
 def adam_step(params, grads, exp_avg, exp_avg_sq, step_i32, lr=1e-3, betas=(0.9, 0.999), eps=1e-7):
     _lib.check(_lib.load().eegnet_adam_step(
         ctypes.c_int64(params.numel()), _ptr(params), _ptr(grads), _ptr(exp_avg), _ptr(exp_avg_sq),

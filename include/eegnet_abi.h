@@ -96,6 +96,15 @@ int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream);
 int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const float* bn_buffers,
                         const float* x, float* logits, void* stream);
 
+/* bf16 batched eval-mode forward (BASELINE cfg5, EEGNet-16,4 at 64ch x 512):
+ * the same function as eegnet_forward_eval (model.py:91-99 in .eval(), called at model.py:161/220,
+ * ui.py:35) on bf16 input x [B,C,T] (16-byte aligned when T % 8 == 0), bf16 MFMA operands and fp32
+ * accumulation; params / bn_buffers / logits as for eegnet_forward_eval (fp32).  Covers every
+ * supported (C, T, F1, D) whose trial fits one workgroup's LDS, including the F2 > 16 shapes the
+ * fp32 train step refuses. */
+int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const float* bn_buffers,
+                             const uint16_t* x, float* logits, void* stream);
+
 /* torch.optim.Adam step (weight_decay 0, amsgrad off) over n elements; `step` is a device int32
  * that is incremented in-kernel (graph-capturable).  torch/optim/adam.py:457,476,531-547. */
 int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_avg,
