@@ -321,7 +321,9 @@ static int make_geo_bf16(const eegnet_dims* d, GeoI* g) {
     g->NT = (g->T + 15) / 16; g->NBLK = (g->NT + 15) / 16;
     g->LPs = g->P + 1;
     g->KSF = (g->K1 + 16 + 31) / 32;
-    g->SXs = rup(256 * g->NBLK + 32 * g->KSF, 64) + 8;
+    // s rows: FIR windows read up to element 256*NBLK + 32*KSF - 16; row stride = 4 mod 8 dwords so the
+    // 16 rows of one spatial-tile store land on distinct bank quads
+    g->SXs = 256 * g->NBLK + 32 * g->KSF - 8;
     g->T1 = g->T / 4; g->T2 = g->T1 / 8; g->NF = g->F2 * g->T2;
     const int nq = (g->T1 + 3) / 4;
     g->RA = 4 * nq + 16;
@@ -344,6 +346,12 @@ static int make_geo_bf16(const eegnet_dims* d, GeoI* g) {
     g->offCo = rup(g->offW2 + g->F2P * K2 * 4, 16);
     g->offL = rup(g->offCo + 4 * g->F2P * 4, 16);
     g->lds = g->offL + NWI * NCLS * 4;
+    // classifier weights staged in LDS when they fit (cfg5: 16 KB), else read from global
+    const int offF = rup(g->lds, 16);
+    if (offF + NCLS * g->NF * 4 <= LDS_MAX) {
+        g->offF = offF;
+        g->lds = offF + NCLS * g->NF * 4;
+    }
     g->dbg = g_bf16_dbg;
     if (g->lds > LDS_MAX)
         return fail(EEGNET_EINVAL, "bf16 eval: dims need %d B of LDS (> %d): C=%d T=%d F2=%d", g->lds, LDS_MAX,

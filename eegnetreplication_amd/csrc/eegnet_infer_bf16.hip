@@ -48,6 +48,7 @@ struct GeoI {
     float eps;
     int o_w1, o_g1, o_b1, o_ws, o_g2, o_b2, o_w2, o_W3, o_g3, o_b3, o_Wfc, o_bfc;
     int offZ, offS, offW1, offW2, offCo, offL, lds;     // LDS carve (bytes)
+    int offF;              // classifier weights [NCLS][NF] fp32 in LDS (0: read from global)
     float* dbg;            // eegnet_debug_bf16: workgroup 0's first trial's s, a, z planes (fp32)
 };
 
@@ -162,6 +163,9 @@ __global__ __launch_bounds__(NTI) void k_infer_bf16(GeoI g, const float* __restr
     for (int i = tid; i < g.F1 * g.K1; i += NTI) W1t[i] = prm[g.o_w1 + i];
     for (int i = tid; i < F2P * K2; i += NTI) W2t[i] = (i / K2) < F2 ? prm[g.o_w2 + i] : 0.f;
     for (int i = tid; i < F2P * g.SXs / 2; i += NTI) reinterpret_cast<unsigned*>(Si)[i] = 0u;
+    float* const Wf = reinterpret_cast<float*>(smi + g.offF);
+    if (g.offF)
+        for (int i = tid; i < NCLS * g.NF; i += NTI) Wf[i] = prm[g.o_Wfc + i];
 
     // spatial GEMM B operand (ws^T, K = c): this wave's 16-row o-tile, all K-steps, in registers
     const int ot = wave % g.NOT, wpo = NWI / g.NOT;
@@ -200,7 +204,7 @@ __global__ __launch_bounds__(NTI) void k_infer_bf16(GeoI g, const float* __restr
     }
     __syncthreads();
 
-    const int rpw = F2P / NWI;                 // FIR rows per wave (>= 2)
+    const int rpw = F2P / NWI;                 // FIR rows per wave (>= 1)
     for (; b < g.B; b += gridDim.x) {
         // ---- 1. spatial GEMM: s^T[t, o] tiles (16 t x 16 o), A = x^T by transposed reads ----
         for (int n = wave / g.NOT; n < g.NT; n += wpo) {
@@ -245,7 +249,9 @@ __global__ __launch_bounds__(NTI) void k_infer_bf16(GeoI g, const float* __restr
                         af[s][j] = (__bf16)((s < g.KSF && k >= 0 && k < g.K1) ? W1t[gg * g.K1 + k] : 0.f);
                     }
             }
-            const float al = Co[o], be = Co[F2P + o];
+            // in log2 units: y = log2(e) * (al v + be); ELU summed over the pool window as
+            // ln2 * sum max(y, 0) + sum exp2(min(y, 0)) - 4 (no per-element compare/select)
+            const float al = Co[o] * 1.4426950408889634f, be = Co[F2P + o] * 1.4426950408889634f;
             const char* srw = Si + o * srow;
             float* arow = Aa + o * g.RA;
             for (int nb = 0; nb < g.NBLK; ++nb) {
@@ -259,11 +265,15 @@ __global__ __launch_bounds__(NTI) void k_infer_bf16(GeoI g, const float* __restr
                     }
                 }
                 // lane: v[o][t = 16n + 4G + r]; pooled sample q = 4n + G
-                float pe = 0.f;
+                float pp = 0.f, pn = 0.f;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) pe += elu_f(fmaf(al, acc[r], be));
+                for (int r = 0; r < 4; ++r) {
+                    const float y = fmaf(al, acc[r], be);
+                    pp += fmaxf(y, 0.f);
+                    pn += __builtin_amdgcn_exp2f(fminf(y, 0.f));
+                }
                 const int q = 4 * n + G;
-                if (q < g.T1) arow[LAI + q] = 0.25f * pe;
+                if (q < g.T1) arow[LAI + q] = fmaf(0.25f * 0.6931471805599453f, pp, 0.25f * pn - 1.f);
             }
             if (lane < LAI) arow[lane] = 0.f;                              // 'same' pad of block_2[0]
             else if (lane < 2 * LAI) arow[LAI + g.T1 + lane - LAI] = 0.f;
@@ -333,7 +343,8 @@ __global__ __launch_bounds__(NTI) void k_infer_bf16(GeoI g, const float* __restr
                     const float hv = 0.125f * e;
                     const int f = j * g.T2 + t2;
 #pragma unroll
-                    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(prm[g.o_Wfc + c * g.NF + f], hv, lp[c]);
+                    for (int c = 0; c < NCLS; ++c)
+                        lp[c] = fmaf(g.offF ? Wf[c * g.NF + f] : prm[g.o_Wfc + c * g.NF + f], hv, lp[c]);
                 }
             }
         }
