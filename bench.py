@@ -131,6 +131,43 @@ def bench_infer_bf16(dev, B, C, T, F1, D, steps, warmup):
     }
 
 
+def bench_folds(dev, n_folds, n_train, epochs):
+    """SURVEY 8(f) row 1 leg: the real training protocol (batch 64, 22 x 257 trials, EEGNet-8,2,
+    p=0.5; train.py:87,229) with n_folds independent cross-subject-sized folds (1,440 training
+    trials each, train.py:182-231) resident at once and advanced in lock-step by FoldBatch, against
+    the same folds trained one after another (the reference's order).  Synthetic data in HBM."""
+    from eegnetreplication_amd import EEGNet, FoldBatch
+    C, T = 22, 257
+    rng = np.random.default_rng(77)
+    X = torch.from_numpy(rng.standard_normal((n_train, C, T), dtype=np.float32)).to(dev)
+    y = torch.from_numpy(rng.integers(0, 4, n_train)).to(dev)
+    torch.manual_seed(3)
+    models = [EEGNet(C, T, p=0.5).to(dev).train() for _ in range(n_folds)]
+
+    def run(batches, ep):
+        gens = [[torch.Generator().manual_seed(100 + k)] for k in range(n_folds)]
+        for fb, ks in batches:                                  # warm-up epoch (workspaces)
+            fb.epoch([(X, y)] * len(ks), 64, [gens[k][0] for k in ks])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(ep):
+            for fb, ks in batches:
+                fb.epoch([(X, y)] * len(ks), 64, [gens[k][0] for k in ks])
+        torch.cuda.synchronize()
+        return n_folds * n_train * ep / (time.perf_counter() - t0)
+
+    ks = list(range(n_folds))
+    graphed = run([(FoldBatch(models, ks, graphs=True), ks)], epochs)
+    together = run([(FoldBatch(models, ks), ks)], epochs)
+    alone = run([(FoldBatch([m], [k]), [k]) for k, m in enumerate(models)], epochs)
+    return {"metric": "real-protocol train trials/sec, batch 64, EEGNet-8,2 22ch x 257",
+            "value": round(graphed, 1), "unit": "trials/s", "folds": n_folds,
+            "train_trials_per_fold": n_train, "epochs": epochs,
+            "mode": "fold-batched: one stream + one captured epoch hipGraph per fold",
+            "eager_concurrent_value": round(together, 1),
+            "sequential_folds_value": round(alone, 1), "speedup": round(graphed / alone, 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,6 +181,8 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-infer", action="store_true", help="skip the cfg5 bf16 inference leg")
     ap.add_argument("--infer-batch", type=int, default=16384)
+    ap.add_argument("--no-folds", action="store_true", help="skip the fold-batched real-protocol leg")
+    ap.add_argument("--folds", type=int, default=16)
     args = ap.parse_args()
 
     from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
@@ -240,6 +279,9 @@ def main():
         infer = None
         if not args.no_infer:
             infer = bench_infer_bf16(dev, args.infer_batch, 64, 512, 16, 4, steps=20, warmup=3)
+        folds = None
+        if not args.no_folds:
+            folds = bench_folds(dev, args.folds, 1440, epochs=2)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             threads = min(16, len(os.sched_getaffinity(0)))
@@ -272,6 +314,7 @@ def main():
             "kernels": per_kernel,
             "final_loss": round(loss, 5),
             "cfg5_infer_bf16": infer,
+            "real_protocol_folds": folds,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

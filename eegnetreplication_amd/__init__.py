@@ -6,6 +6,7 @@ The compute runs in ``libeegnet_hip.so`` (hand-written gfx950 HIP kernels, C-ABI
 """
 
 from .model import EEGNet, FusedTrainer, evaluate_model, train  # noqa: F401
+from .folds import FoldBatch  # noqa: F401
 from .ops import Shape  # noqa: F401
 
-__all__ = ["EEGNet", "FusedTrainer", "Shape", "evaluate_model", "train"]
+__all__ = ["EEGNet", "FoldBatch", "FusedTrainer", "Shape", "evaluate_model", "train"]

@@ -50,6 +50,9 @@ struct Geo {
     unsigned long long key;
     unsigned key0, key1;  // per-layer 32-bit dropout keys (derived from key)
     unsigned pthr;        // dropout threshold p * 2^24
+    // graph-replayable keys (EEGNET_KEY_FROM_STEP): key = mix(kseed, koff + *keystep), read on device
+    const int32_t* keystep;
+    unsigned long long kseed, koff;
     // flat parameter offsets (named_parameters order)
     int o_w1, o_g1, o_b1, o_ws, o_g2, o_b2, o_w2, o_W3, o_g3, o_b3, o_Wfc, o_bfc, nparam;
     // partial-row lengths of the five passes and the (common) workgroup count
@@ -211,11 +214,27 @@ __device__ __forceinline__ float elu_d(float z) { return z > 0.f ? 1.f : fast_ex
 // Dropout keep factor (model.py:50,74 nn.Dropout: x * mask / (1-p)).  Injected masks win; otherwise a
 // counter-based draw: murmur3's 32-bit finalizer of (flat index * golden ratio + per-layer key), top
 // 24 bits against p * 2^24.  Identical in forward and backward, a few VALU ops per element.
-__device__ __forceinline__ float keep_mul(const Geo& g, const uint8_t* __restrict__ mask, int layer,
+// splitmix64 finalizer of (seed, offset): the host's mix_key (eegnet_host.hip), restated for keys
+// read on the device
+__device__ __forceinline__ unsigned long long mix_key_dev(unsigned long long seed, unsigned long long off) {
+    unsigned long long z = seed * 0xD1B54A32D192ED03ull + off * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// per-layer 32-bit dropout key of this call, hoisted to kernel entry by the passes that draw masks.
+// With keystep set (graph replays) the offset advances with the device Adam step, which only pass
+// E's finalize increments -- after every reader of this step has run.
+__device__ __forceinline__ unsigned drop_key(const Geo& g, int layer) {
+    if (!g.keystep) return layer ? g.key1 : g.key0;
+    const unsigned long long k = mix_key_dev(g.kseed, g.koff + (unsigned long long)(*g.keystep));
+    return layer ? (unsigned)(k >> 32) ^ 0x5BD1E995u : (unsigned)k;
+}
+__device__ __forceinline__ float keep_mul(const Geo& g, const uint8_t* __restrict__ mask, unsigned key,
                                           unsigned idx) {
     if (!g.drop) return 1.f;
     if (mask) return mask[idx] ? g.scale : 0.f;
-    unsigned h = idx * 0x9E3779B1u + (layer ? g.key1 : g.key0);
+    unsigned h = idx * 0x9E3779B1u + key;
     h ^= h >> 16;
     h *= 0x85EBCA6Bu;
     h ^= h >> 13;

@@ -502,6 +502,10 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
     g.drop = g.p > 0.f ? 1 : 0;
     set_key(&g, seed, offset);
+    if (flags & EEGNET_KEY_FROM_STEP) {
+        if (!step) return fail(EEGNET_EINVAL, "EEGNET_KEY_FROM_STEP needs the device step counter");
+        g.keystep = step; g.kseed = seed; g.koff = offset;
+    }
     ensure_attrs();
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;

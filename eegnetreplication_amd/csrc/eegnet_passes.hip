@@ -206,6 +206,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
                                                 float* __restrict__ part, int mode, FinArgs fa) {
     EEG_DIMS(g);
     TRACE(g, 2, TR_ENTRY);
+    const unsigned dk1 = drop_key(g, 1);
     constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
     constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
     const int NFP = rup4(NF);
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
 #pragma unroll
         for (int u = 0; u < NFQ; ++u) {
             const int i = lane + 64 * u;
-            kp[u] = i < NF ? keep_mul(g, mask3, 1, (unsigned)(b * NF + i)) : 0.f;
+            kp[u] = i < NF ? keep_mul(g, mask3, dk1, (unsigned)(b * NF + i)) : 0.f;
             hv[u] = i < NF ? Hs[i] * kp[u] : 0.f;          // dropout (model.py:74)
         }
         // logits (model.py:78-82)
@@ -394,6 +395,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                                                  FinArgs fa) {
     EEG_DIMS(g);
     TRACE(g, 3, TR_ENTRY);
+    const unsigned dk0 = drop_key(g, 0), dk1 = drop_key(g, 1);
     constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
     constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
     const int RSW = TT ? row_stride_b2(TT / 4) : g.RSW;
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             float dd = 0.f;
 #pragma unroll
             for (int n = 0; n < NCLS; ++n) dd = fmaf(dlv[n], wf[n][u], dd);
-            if (i < NF) Hs[i] = dd * keep_mul(g, mask3, 1, (unsigned)(b * NF + i));
+            if (i < NF) Hs[i] = dd * keep_mul(g, mask3, dk1, (unsigned)(b * NF + i));
         }
         float q[F2MAX][MQ];
         dwconv_rows<MQ>(g, prm, F2, d, lane, q);
@@ -558,7 +560,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                 const int t = lane + 64 * m;
                 if (t < T1) {
                     const int gi = o * T1 + t;
-                    const float dp = a[m] * keep_mul(g, mask2, 0, (unsigned)(rb + gi));
+                    const float dp = a[m] * keep_mul(g, mask2, dk0, (unsigned)(rb + gi));
                     dp2g[rb + gi] = dp;
                     sz[o] = fmaf(dp * 0.25f, e1v[o][m], sz[o]);
                     sz[F2MAX + o] = fmaf(dp * 0.25f, e2v[o][m], sz[F2MAX + o]);

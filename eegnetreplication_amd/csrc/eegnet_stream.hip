@@ -304,6 +304,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 1, TR_ENTRY);
+    const unsigned dk0 = drop_key(g, 0);
     constexpr int NTS = FF ? 1 : RPW;
     const int D = FF ? 2 : g.D;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
                             e1 += dz;
                             e2 = fmaf(dz, xh, e2);
                         }
-                        const float d2 = q < T1 ? pe * 0.25f * keep_mul(g, mask2, 0, (unsigned)((b * F2 + oh) * T1 + q)) : 0.f;
+                        const float d2 = q < T1 ? pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)((b * F2 + oh) * T1 + q)) : 0.f;
                         d2v[m][h] = d2; e1v[m][h] = e1; e2v[m][h] = e2;
                         if (q < T1) drow[q] = d2;
                     }

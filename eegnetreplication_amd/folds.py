@@ -1,0 +1,122 @@
+"""Fold-batched training: k independent EEGNet fold runs advanced in lock-step on one GPU
+(SURVEY.md 8(f) row 1).
+
+The real protocol trains at batch 64 (train.py:87,229): one fused step is a few microseconds of
+work spread over a handful of small launches, so a single fold leaves most of the 256 CUs idle
+and the host waits on every launch.  The within-subject protocol has 36 independent runs and the
+cross-subject one 90 (train.py:50,73,182,194).  ``FoldBatch`` keeps k of them resident (own
+parameters, BN buffers, Adam state and workspace each) and enqueues step j of every fold before
+step j+1 of any, each fold on its own HIP stream, so the kernels of different folds overlap on
+the device and no host synchronisation happens inside an epoch.
+
+Per fold the arithmetic is exactly ``FusedTrainer.step`` (model.py:141-148 semantics: forward,
+CE, backward with the two clamps, Adam); only the interleaving changes.  Dropout keys are
+counter-based per fold -- (fold seed, step counter) -- so a fold's trajectory does not depend on
+how many other folds run beside it (tests/test_gpu_folds.py checks bit-equality with the same fold
+run alone).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from .model import EEGNet, FusedAdamState
+
+
+class _FoldGraph:
+    """One fold's captured epoch: static permutation and per-step loss slots, and the graph."""
+
+    def __init__(self, X, n, batch_size, perm, losses, graph):
+        self.X, self.n, self.batch_size = X, n, batch_size
+        self.perm, self.losses, self.graph = perm, losses, graph
+
+
+class FoldBatch:
+    """k independent fold runs on one GPU, one HIP stream each.
+
+    ``graphs=True`` captures each fold's epoch (batch gathers + fused steps) as a hipGraph after
+    its first, eager epoch and replays it afterwards: one host call per fold per epoch instead of
+    ~10 launches per step.  Dropout keys follow the device Adam step (EEGNET_KEY_FROM_STEP) in both
+    modes, so replays draw fresh masks each step and graph and eager runs are bit-identical."""
+
+    def __init__(self, models: list[EEGNet], seeds: list[int], lr=1e-3, betas=(0.9, 0.999),
+                 eps=1e-7, graphs=False):
+        if len(models) != len(seeds) or not models:
+            raise ValueError("need one seed per model and at least one model")
+        dev = models[0].flat_parameters().device
+        if dev.type != "cuda":
+            raise RuntimeError("FoldBatch runs on a HIP device only")
+        self.models = models
+        self.seeds = [int(s) for s in seeds]
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.graphs = graphs
+        self.adam = [FusedAdamState(m) for m in models]
+        self.streams = [torch.cuda.Stream(device=dev) for _ in models]
+        self._ws: list[dict] = [{} for _ in models]
+        self._graph: list[_FoldGraph | None] = [None] * len(models)
+
+    def __len__(self):
+        return len(self.models)
+
+    def _workspace(self, k, B):
+        ws = self._ws[k].get(B)
+        if ws is None:
+            ws = ops.new_workspace(self.models[k].shape, B, self.models[k].flat_parameters().device)
+            self._ws[k][B] = ws
+        return ws
+
+    def _steps(self, k, X, y, perm, losses, batch_size):
+        """Enqueue one epoch of fold k on the current stream: batch j is X[perm[jB:(j+1)B]] and
+        its loss lands in losses[j] (no accumulation kernel)."""
+        m = self.models[k]
+        a = self.adam[k]
+        for j, i in enumerate(range(0, perm.shape[0], batch_size)):
+            idx = perm[i:i + batch_size]
+            xb, yb = X.index_select(0, idx), y.index_select(0, idx)
+            ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), xb, yb, self.seeds[k],
+                           0, a.grads, a.state, a.step, self._workspace(k, xb.shape[0]),
+                           losses[j:j + 1], lr=self.lr, betas=self.betas, eps=self.eps,
+                           nbt=m.flat_num_batches_tracked(), key_from_step=True)
+
+    def epoch(self, data: list[tuple[torch.Tensor, torch.Tensor]], batch_size: int = 64,
+              generators: list[torch.Generator] | None = None) -> list[torch.Tensor]:
+        """One training epoch of every fold.  ``data[k] = (X_k [N_k,C,T] fp32, y_k [N_k] int64)``,
+        device-resident.  Each fold is shuffled by its own generator (DataLoader(shuffle=True),
+        train.py:87) and cut into batches of ``batch_size`` with a short last batch
+        (drop_last=False).  Returns per-fold float64 device scalars: the sum of the batch losses
+        (the reference's running loss, model.py:150).  Nothing is synchronised."""
+        if len(data) != len(self.models):
+            raise ValueError("one (X, y) per fold")
+        cur = torch.cuda.current_stream()
+        sums = []
+        for k, (X, y) in enumerate(data):
+            n = X.shape[0]
+            nsteps = (n + batch_size - 1) // batch_size
+            g = generators[k] if generators is not None else None
+            perm = torch.randperm(n, generator=g) if g is not None else torch.arange(n)
+            s = self.streams[k]
+            s.wait_stream(cur)
+            st = self._graph[k]
+            with torch.cuda.stream(s):
+                if st is not None and st.X is X and st.n == n and st.batch_size == batch_size:
+                    st.perm.copy_(perm, non_blocking=True)
+                    st.graph.replay()
+                    sums.append(st.losses.sum(dtype=torch.float64))
+                    continue
+                perm_d = perm.to(X.device)
+                losses = torch.zeros(nsteps, dtype=torch.float32, device=X.device)
+                self._steps(k, X, y, perm_d, losses, batch_size)
+                sums.append(losses.sum(dtype=torch.float64))
+                if self.graphs:                 # capture for the next epochs (workspaces exist now)
+                    gr = torch.cuda.CUDAGraph()
+                    sperm = perm_d.clone()
+                    slosses = torch.zeros_like(losses)
+                    with torch.cuda.graph(gr, stream=s):
+                        self._steps(k, X, y, sperm, slosses, batch_size)
+                    self._graph[k] = _FoldGraph(X, n, batch_size, sperm, slosses, gr)
+        for s in self.streams:
+            cur.wait_stream(s)
+        for t in sums:
+            t.record_stream(cur)
+        return sums

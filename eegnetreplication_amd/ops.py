@@ -109,6 +109,7 @@ def forward_train(shape: Shape, flat_params, bn_flat, x, ws, seed: int, offset: 
 
 
 NO_CLAMP = 1
+KEY_FROM_STEP = 2      # include/eegnet_abi.h: dropout key follows the device Adam step (graphs)
 
 
 def backward(shape: Shape, flat_params, x, ws, seed: int, offset: int, dlogits=None, labels=None,
@@ -164,7 +165,7 @@ def adam_step(params, grads, exp_avg, exp_avg_sq, step_i32, lr=1e-3, betas=(0.9,
 
 def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset: int, grads,
                adam_state, step_i32, ws, loss, logits=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-7,
-               p: float | None = None, clamp=True, nbt=None):
+               p: float | None = None, clamp=True, nbt=None, key_from_step=False):
     """One fused hot-loop iteration (model.py:141-148) on the device, no host sync.
     ``adam_state=None`` stops after the gradients (data-parallel)."""
     d = shape.dims(x.shape[0], p)
@@ -173,4 +174,5 @@ def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset:
         ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),
         _ptr(step_i32), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
         ctypes.c_float(eps), _ptr(loss), _ptr(logits), _ptr(ws), _stream(),
-        0 if clamp else NO_CLAMP, _ptr(nbt)), "eegnet_train_step")
+        (0 if clamp else NO_CLAMP) | (KEY_FROM_STEP if key_from_step else 0), _ptr(nbt)),
+        "eegnet_train_step")

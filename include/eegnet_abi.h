@@ -59,7 +59,11 @@ enum {
 enum { EEGNET_TRAIN = 1, EEGNET_EVAL = 0 };
 
 /* eegnet_backward flags */
-enum { EEGNET_NO_CLAMP = 1 /* leave model.py:44/84 clamps to eegnet_clamp_grads (after an all-reduce) */ };
+enum {
+    EEGNET_NO_CLAMP = 1,      /* leave model.py:44/84 clamps to eegnet_clamp_grads (after an all-reduce) */
+    EEGNET_KEY_FROM_STEP = 2  /* eegnet_train_step: dropout key = mix(seed, offset + *step), read on the
+                                 device, so a captured hipGraph draws fresh masks on every replay */
+};
 
 /* Number of fp32 elements of the flat parameter buffer for these dims. */
 int eegnet_param_count(const eegnet_dims* dims, int64_t* out);
@@ -114,7 +118,8 @@ int eegnet_adam_step(int64_t n, float* params, const float* grads, float* exp_av
 /* One fused hot-loop iteration (model.py:141-148): forward_train + CE + backward + clamps + Adam.
  * adam_state = [exp_avg | exp_avg_sq] (2 * param_count floats); step as in eegnet_adam_step.
  * adam_state == NULL stops after the gradients (data-parallel callers all-reduce them, then call
- * eegnet_clamp_grads and eegnet_adam_step); flags as for eegnet_backward.  logits is nullable. */
+ * eegnet_clamp_grads and eegnet_adam_step); flags as for eegnet_backward, plus EEGNET_KEY_FROM_STEP
+ * (needs step; the mask key then follows the device step, for hipGraph capture).  logits is nullable. */
 int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers, const float* x,
                       const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
                       float* adam_state, int32_t* step, float lr, float beta1, float beta2,

@@ -1,0 +1,138 @@
+"""Fold-batched training (eegnetreplication_amd.folds.FoldBatch) on the GPU.
+
+FoldBatch only interleaves independent fused steps over HIP streams, so the bar is bit-equality:
+every fold of a concurrent batch must end with exactly the parameters, BN buffers, Adam state and
+loss sums of the same fold trained alone, and a one-fold batch must reproduce FusedTrainer, whose
+step is pinned to the oracle and the reference golden vectors by tests/test_gpu_parity.py.
+Shapes follow the real protocol: 22 x 257 trials (02_preprocessing_pipeline.ipynb:1867), batch 64
+with a short last batch (train.py:87, DataLoader drop_last=False).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+C, T = 22, 257
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _data(n, seed, dev):
+    rng = np.random.default_rng(seed)
+    X = torch.from_numpy(rng.standard_normal((n, C, T), dtype=np.float32)).to(dev)
+    y = torch.from_numpy(rng.integers(0, 4, n).astype(np.int64)).to(dev)
+    return X, y
+
+
+def _models(k, p, dev):
+    from eegnetreplication_amd import EEGNet
+    torch.manual_seed(7)
+    out = []
+    for _ in range(k):
+        out.append(EEGNet(C, T, p=p).to(dev))
+    return out
+
+
+def _clone(m, p, dev):
+    from eegnetreplication_amd import EEGNet
+    c = EEGNet(C, T, p=p)
+    c.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    return c.to(dev)
+
+
+def _state(fb, k):
+    m = fb.models[k]
+    return (m.flat_parameters().clone(), m.flat_bn_buffers().clone(), fb.adam[k].state.clone(),
+            m.flat_num_batches_tracked().clone())
+
+
+def test_concurrent_folds_equal_each_fold_alone():
+    from eegnetreplication_amd import FoldBatch
+    dev = _dev()
+    sizes, seeds = [200, 130, 69], [11, 22, 33]
+    data = [_data(n, 100 + i, dev) for i, n in enumerate(sizes)]
+    models = _models(3, 0.5, dev)
+    alone = [_clone(m, 0.5, dev) for m in models]
+    fb = FoldBatch(models, seeds)
+    gens = [torch.Generator().manual_seed(s) for s in seeds]
+    sums_all = [fb.epoch(data, 64, gens) for _ in range(2)]
+    torch.cuda.synchronize()
+    for k in range(3):
+        one = FoldBatch([alone[k]], [seeds[k]])
+        g = [torch.Generator().manual_seed(seeds[k])]
+        sums_one = [one.epoch([data[k]], 64, g) for _ in range(2)]
+        torch.cuda.synchronize()
+        for a, b in zip(_state(fb, k), _state(one, 0)):
+            assert torch.equal(a, b), f"fold {k}: concurrent run differs from the fold alone"
+        for e in range(2):
+            assert torch.equal(sums_all[e][k], sums_one[e][0]), f"fold {k} epoch {e}: loss sums differ"
+        assert np.isfinite(float(sums_one[1][0]))
+        assert int(fb.adam[k].step.item()) == 2 * ((sizes[k] + 63) // 64)
+
+
+def test_single_fold_matches_fused_trainer():
+    from eegnetreplication_amd import FoldBatch, FusedTrainer
+    dev = _dev()
+    X, y = _data(150, 5, dev)
+    (m,) = _models(1, 0.0, dev)           # p = 0: the dropout key stream does not matter
+    ref = _clone(m, 0.0, dev)
+    fb = FoldBatch([m], [1])
+    fb.epoch([(X, y)], 64, [torch.Generator().manual_seed(3)])
+    perm = torch.randperm(150, generator=torch.Generator().manual_seed(3)).to(dev)
+    tr = FusedTrainer(ref)
+    for i in range(0, 150, 64):
+        idx = perm[i:i + 64]
+        tr.step(X.index_select(0, idx), y.index_select(0, idx))
+    torch.cuda.synchronize()
+    assert torch.equal(m.flat_parameters(), ref.flat_parameters())
+    assert torch.equal(m.flat_bn_buffers(), ref.flat_bn_buffers())
+    assert torch.equal(fb.adam[0].state, tr.adam.state)
+
+
+def test_graph_replay_equals_eager():
+    """graphs=True: epoch 1 eager + capture, later epochs replay the captured graph.  Dropout keys
+    follow the device step, so replays must match an all-eager run bit for bit."""
+    from eegnetreplication_amd import FoldBatch
+    dev = _dev()
+    sizes, seeds = [150, 100], [5, 6]
+    data = [_data(n, 200 + i, dev) for i, n in enumerate(sizes)]
+    models = _models(2, 0.5, dev)
+    twins = [_clone(m, 0.5, dev) for m in models]
+    eager = FoldBatch(models, seeds)
+    graph = FoldBatch(twins, seeds, graphs=True)
+    ge = [torch.Generator().manual_seed(s) for s in seeds]
+    gg = [torch.Generator().manual_seed(s) for s in seeds]
+    for e in range(3):
+        se = eager.epoch(data, 64, ge)
+        sg = graph.epoch(data, 64, gg)
+        torch.cuda.synchronize()
+        for k in range(2):
+            assert torch.equal(se[k], sg[k]), f"epoch {e} fold {k}: loss sums differ"
+            for a, b in zip(_state(eager, k), _state(graph, k)):
+                assert torch.equal(a, b), f"epoch {e} fold {k}: graph replay differs from eager"
+    assert all(graph._graph[k] is not None for k in range(2))
+    assert int(graph.adam[0].step.item()) == 3 * 3
+
+
+def test_step_keyed_dropout_changes_every_step():
+    """With keys from the device step, a replayed step must not reuse the previous step's masks:
+    two steps on the same batch from the same weights differ only through the step counter."""
+    from eegnetreplication_amd import FoldBatch
+    dev = _dev()
+    X, y = _data(64, 9, dev)
+    (m,) = _models(1, 0.5, dev)
+    a, b = _clone(m, 0.5, dev), _clone(m, 0.5, dev)
+    fa, fb = FoldBatch([a], [1]), FoldBatch([b], [1])
+    fb.adam[0].step.fill_(1)               # same weights and moments, next step's key
+    la = fa.epoch([(X, y)], 64)[0]
+    lb = fb.epoch([(X, y)], 64)[0]
+    torch.cuda.synchronize()
+    assert not torch.equal(la, lb), "dropout masks did not change with the step counter"
