@@ -67,13 +67,14 @@ class FoldBatch:
         return ws
 
     def _steps(self, k, X, y, perm, losses, batch_size):
-        """Enqueue one epoch of fold k on the current stream: batch j is X[perm[jB:(j+1)B]] and
-        its loss lands in losses[j] (no accumulation kernel)."""
+        """Enqueue one epoch of fold k on the current stream: the epoch's shuffled copy of X is
+        gathered once (one launch, not two per step), batch j is its rows [jB, (j+1)B), and its
+        loss lands in losses[j] (no accumulation kernel)."""
         m = self.models[k]
         a = self.adam[k]
+        Xp, yp = X.index_select(0, perm), y.index_select(0, perm)
         for j, i in enumerate(range(0, perm.shape[0], batch_size)):
-            idx = perm[i:i + batch_size]
-            xb, yb = X.index_select(0, idx), y.index_select(0, idx)
+            xb, yb = Xp[i:i + batch_size], yp[i:i + batch_size]
             ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), xb, yb, self.seeds[k],
                            0, a.grads, a.state, a.step, self._workspace(k, xb.shape[0]),
                            losses[j:j + 1], lr=self.lr, betas=self.betas, eps=self.eps,
