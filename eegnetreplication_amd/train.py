@@ -65,6 +65,71 @@ def _run_fold(X, y, tr_ids, va_ids, te, p, epochs, seed, device):
             "state": {k: v.detach().cpu() for k, v in best.items()}}
 
 
+def _run_folds(specs, epochs, device):
+    """Several independent units trained together by FoldBatch:
+    per-fold streams, one captured hipGraph per fold epoch, no host sync until the end.  Each
+    spec is _run_fold's arguments (X, y, tr_ids, va_ids, te, p, seed).  Per fold and epoch, as in
+    train() (model.py:101-189): the train loss is the mean of the batch losses, the validation
+    loss the mean of per-batch CE means over batches of 64, the validation accuracy over all
+    validation trials; the returned state is the final weights (the reference's aliasing "best",
+    SURVEY F4).  Returns one result dict per spec, like _run_fold."""
+    import torch.nn.functional as F
+    from .folds import FoldBatch
+    models, seeds, train_sets, val_sets, test_sets, gens = [], [], [], [], [], []
+    for X, y, tr_ids, va_ids, te, p, seed in specs:
+        torch.manual_seed(seed)
+        models.append(EEGNet(C=X.shape[1], T=X.shape[2], p=p).to(device))
+        seeds.append(seed)
+        gens.append(torch.Generator().manual_seed(seed))
+
+        def dev(a, dt):
+            return torch.as_tensor(np.asarray(a), dtype=dt).to(device)
+        train_sets.append((dev(X[tr_ids], torch.float32), dev(y[tr_ids], torch.int64)))
+        val_sets.append((dev(X[va_ids], torch.float32), dev(y[va_ids], torch.int64)))
+        test_sets.append((dev(te[0], torch.float32), dev(te[1], torch.int64)))
+    fb = FoldBatch(models, seeds, graphs=True)
+    val_loss = [[] for _ in specs]
+    val_acc = [[] for _ in specs]
+    for e in range(1, epochs + 1):
+        fb.epoch(train_sets, BATCH_SIZE, gens)
+        with torch.no_grad():
+            for k, (m, (Xv, yv)) in enumerate(zip(models, val_sets)):
+                m.eval()
+                logits = m(Xv)                      # eval BN: batch-size independent
+                m.train()
+                ce = F.cross_entropy(logits, yv, reduction="none")
+                nb = (len(yv) + BATCH_SIZE - 1) // BATCH_SIZE
+                seg = torch.arange(len(yv), device=ce.device) // BATCH_SIZE
+                means = torch.zeros(nb, dtype=torch.float64, device=ce.device).index_add_(
+                    0, seg, ce.double()) / torch.bincount(seg, minlength=nb).double()
+                val_loss[k].append(means.mean())
+                val_acc[k].append((logits.argmax(1) == yv).sum())
+        if e == 1 or e % 50 == 0 or e == epochs:
+            logger.info(f"Epoch: {e}/{epochs} ({len(specs)} folds batched)")
+    out = []
+    for k, m in enumerate(models):
+        m.eval()
+        Xt, yt = test_sets[k]
+        with torch.no_grad():
+            correct = int((m(Xt).argmax(1) == yt).sum().item())
+        vl = torch.stack(val_loss[k]).cpu().numpy()
+        va = 100.0 * torch.stack(val_acc[k]).cpu().numpy() / len(val_sets[k][1])
+        out.append({"test_acc": 100 * correct / len(yt), "val_acc": float(va.max()),
+                    "val_loss": float(vl.min()),
+                    "state": {n: v.detach().cpu() for n, v in m.state_dict().items()}})
+    return out
+
+
+def _run_units(specs, epochs, device, fold_batch):
+    """Run unit specs one by one (_run_fold) or fold_batch at a time (_run_folds)."""
+    if fold_batch <= 1:
+        return [_run_fold(*sp[:5], sp[5], epochs, sp[6], device) for sp in specs]
+    res = []
+    for i in range(0, len(specs), fold_batch):
+        res.extend(_run_folds(specs[i:i + fold_batch], epochs, device))
+    return res
+
+
 def within_subject_units():
     units = []
     for s in range(1, N_SUBJECTS + 1):
@@ -73,12 +138,13 @@ def within_subject_units():
     return units
 
 
-def within_subject_training(epochs=EPOCHS, seed=0, device="cuda"):
-    """train.py:30-148.  Returns (per_subject_test_acc, avg_test_acc, best_model_states)."""
+def within_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0):
+    """train.py:30-148.  Returns (per_subject_test_acc, avg_test_acc, best_model_states).
+    ``fold_batch`` > 1 trains that many of this rank's units together (FoldBatch)."""
     rank, world, _ = D.env_rank_world()
     units = within_subject_units()
     mine = D.lpt_assign([1.0] * len(units), world)[rank] if world > 1 else range(len(units))
-    cache, local = {}, {}
+    cache, local, specs = {}, {}, []
     for u in mine:
         s, f = units[u]
         if s not in cache:
@@ -91,8 +157,10 @@ def within_subject_training(epochs=EPOCHS, seed=0, device="cuda"):
         train_val, test_ids = splits[f]
         nval = len(train_val) // 5
         logger.info(f"Subject {s} fold {f + 1}/4 on rank {rank}")
-        local[u] = _run_fold(data.X, data.y, train_val[nval:], train_val[:nval],
-                             (data.X[test_ids], data.y[test_ids]), 0.5, epochs, seed + u, device)
+        specs.append((data.X, data.y, train_val[nval:], train_val[:nval],
+                      (data.X[test_ids], data.y[test_ids]), 0.5, seed + u))
+    for u, r in zip(mine, _run_units(specs, epochs, device, fold_batch)):
+        local[u] = r
     res = D.gather_results(local)
     per_subject, states = [], []
     for s in range(1, N_SUBJECTS + 1):
@@ -121,8 +189,9 @@ def cross_subject_units():
     return units
 
 
-def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda"):
-    """train.py:151-291.  Returns (best_model_state, per_subject_test_acc, avg_test_acc)."""
+def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0):
+    """train.py:151-291.  Returns (best_model_state, per_subject_test_acc, avg_test_acc).
+    ``fold_batch`` > 1 trains that many of this rank's folds together (FoldBatch)."""
     rank, world, _ = D.env_rank_world()
     units = cross_subject_units()
     mine = D.lpt_assign([1.0] * len(units), world)[rank] if world > 1 else range(len(units))
@@ -133,7 +202,7 @@ def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda"):
             sessions[(s, mode)] = build_dataset_from_preprocessed(subject=s, mode=mode)
         return sessions[(s, mode)]
 
-    local = {}
+    local, specs = {}, []
     for u in mine:
         s, k, trs, vas = units[u]
         X = np.concatenate([sess(v, "Train").X for v in trs + vas])
@@ -142,7 +211,9 @@ def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda"):
         ids = np.arange(len(y))
         te = sess(s, "Eval")
         logger.info(f"Fold {k}/90 (Subject {s}) on rank {rank}")
-        local[u] = _run_fold(X, y, ids[:ntr], ids[ntr:], (te.X, te.y), 0.25, epochs, seed + u, device)
+        specs.append((X, y, ids[:ntr], ids[ntr:], (te.X, te.y), 0.25, seed + u))
+    for u, r in zip(mine, _run_units(specs, epochs, device, fold_batch)):
+        local[u] = r
     res = D.gather_results(local)
     per_subject, all_acc = [], []
     best_loss, best_state = 100, None
@@ -250,6 +321,8 @@ def main(argv=None) -> None:
     ap.add_argument("--generateReport", type=bool, default=True, help="Generate report after training.")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", type=str, default=".", help="directory for models/ and reports/")
+    ap.add_argument("--fold-batch", type=int, default=16,
+                    help="train this many folds together on one GPU (FoldBatch); 0/1: one at a time")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO,
                         format="%(asctime)s - %(filename)s - %(funcName)s - %(levelname)s - %(message)s",
@@ -260,7 +333,7 @@ def main(argv=None) -> None:
     models_dir = os.path.join(args.out, "models")
     reports_dir = os.path.join(args.out, "reports")
     if args.trainingType == "Within-Subject":
-        per_subject, avg, states = within_subject_training(args.epochs, args.seed, device)
+        per_subject, avg, states = within_subject_training(args.epochs, args.seed, device, args.fold_batch)
         if rank == 0:
             os.makedirs(models_dir, exist_ok=True)
             for s, st in enumerate(states, 1):
@@ -268,7 +341,7 @@ def main(argv=None) -> None:
             if args.generateReport:
                 generate_ws_report(per_subject, avg, states, reports_dir)
     else:
-        best, per_subject, avg = cross_subject_training(args.epochs, args.seed, device)
+        best, per_subject, avg = cross_subject_training(args.epochs, args.seed, device, args.fold_batch)
         if rank == 0:
             os.makedirs(models_dir, exist_ok=True)
             torch.save(best, os.path.join(models_dir, "cross_subject_best_model.pth"))

@@ -136,3 +136,29 @@ def test_step_keyed_dropout_changes_every_step():
     lb = fb.epoch([(X, y)], 64)[0]
     torch.cuda.synchronize()
     assert not torch.equal(la, lb), "dropout masks did not change with the step counter"
+
+
+def test_protocol_fold_batch_matches_one_at_a_time():
+    """train.py's protocol runner: _run_folds (FoldBatch, graphs) against _run_fold (the
+    reference-shaped train() + evaluate_model() loop, model.py:101-227) on the same units.  With
+    p = 0 the dropout keying is moot, so the trained weights must agree bit for bit and the
+    reported accuracies exactly; validation losses agree to fp32 rounding (batch-mean order)."""
+    import importlib
+    T_ = importlib.import_module("eegnetreplication_amd.train")   # (the package exports train())
+    dev = _dev()
+    rng = np.random.default_rng(4)
+    specs = []
+    for u in range(3):
+        X = rng.standard_normal((150, C, T)).astype(np.float64)
+        y = rng.integers(0, 4, 150).astype(np.int64)
+        ids = rng.permutation(150)
+        te = (rng.standard_normal((40, C, T)), rng.integers(0, 4, 40).astype(np.int64))
+        specs.append((X, y, ids[:100], ids[100:], te, 0.0, 10 + u))
+    batched = T_._run_units(specs, 3, dev, fold_batch=3)
+    single = T_._run_units(specs, 3, dev, fold_batch=0)
+    for k, (a, b) in enumerate(zip(batched, single)):
+        assert a["test_acc"] == b["test_acc"], k
+        assert a["val_acc"] == b["val_acc"], k
+        assert abs(a["val_loss"] - b["val_loss"]) <= 1e-5 * abs(b["val_loss"]), k
+        for n in b["state"]:
+            assert torch.equal(a["state"][n], b["state"][n]), f"unit {k}: {n} differs"
