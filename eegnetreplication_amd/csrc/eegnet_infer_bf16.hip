@@ -207,16 +207,39 @@ __global__ __launch_bounds__(NTI) void k_infer_bf16(GeoI g, const float* __restr
     const int rpw = F2P / NWI;                 // FIR rows per wave (>= 1)
     for (; b < g.B; b += gridDim.x) {
         // ---- 1. spatial GEMM: s^T[t, o] tiles (16 t x 16 o), A = x^T by transposed reads ----
-        for (int n = wave / g.NOT; n < g.NT; n += wpo) {
-            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-            acc = mfma_bf16(tr_frag(Xi, xrow, 0, 16 * n, lane), wsf[0], acc);
-            if (g.KC > 1) acc = mfma_bf16(tr_frag(Xi, xrow, 32, 16 * n, lane), wsf[1], acc);
+        // two t-tiles per iteration: all transposed reads issue before the first MFMA (the s
+        // stores of the previous iteration may alias Xi as far as the compiler knows)
+        auto s_store = [&](const floatx4& acc, int n) {
             // lane: s[o = ot*16 + l15][t = 16n + 4G + r], r = 0..3 -> one 8-byte store
             const int o = ot * 16 + l15;
             uintx2 pk;
             pk[0] = pack_bf16x2(acc[0], acc[1]);
             pk[1] = pack_bf16x2(acc[2], acc[3]);
             *reinterpret_cast<uintx2*>(Si + o * srow + 2 * (g.LPs + 16 * n + 4 * G)) = pk;
+        };
+        int n = wave / g.NOT;
+        for (; n + wpo < g.NT; n += 2 * wpo) {
+            const int n1 = n + wpo;
+            const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
+            if (g.KC > 1) {
+                const bf16x8 a00 = tr_frag(Xi, xrow, 0, 16 * n, lane), a10 = tr_frag(Xi, xrow, 0, 16 * n1, lane);
+                const bf16x8 a01 = tr_frag(Xi, xrow, 32, 16 * n, lane), a11 = tr_frag(Xi, xrow, 32, 16 * n1, lane);
+                floatx4 c0 = mfma_bf16(a00, wsf[0], z4), c1 = mfma_bf16(a10, wsf[0], z4);
+                c0 = mfma_bf16(a01, wsf[1], c0);
+                c1 = mfma_bf16(a11, wsf[1], c1);
+                s_store(c0, n);
+                s_store(c1, n1);
+            } else {
+                const bf16x8 a00 = tr_frag(Xi, xrow, 0, 16 * n, lane), a10 = tr_frag(Xi, xrow, 0, 16 * n1, lane);
+                s_store(mfma_bf16(a00, wsf[0], z4), n);
+                s_store(mfma_bf16(a10, wsf[0], z4), n1);
+            }
+        }
+        if (n < g.NT) {
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            acc = mfma_bf16(tr_frag(Xi, xrow, 0, 16 * n, lane), wsf[0], acc);
+            if (g.KC > 1) acc = mfma_bf16(tr_frag(Xi, xrow, 32, 16 * n, lane), wsf[1], acc);
+            s_store(acc, n);
         }
         __syncthreads();
         const bool dump = g.dbg != nullptr && b == 0;
