@@ -117,6 +117,11 @@ def bench_infer_bf16(dev, B, C, T, F1, D, steps, warmup):
         kern = _lib.profile_collect()
         _lib.profile_enable(False)
     cnt, tot = kern.get("k_infer_bf16", (0, 0.0))
+    traffic = None                    # HBM bytes per launch from the committed rocprofv3 PMC passes
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path) and B == 16384:
+        with open(pmc_path) as f:
+            traffic = json.load(f).get("k_infer_bf16", {}).get("hbm_bytes_per_launch")
     avg_s = tot / max(cnt, 1) * 1e-3
     by, fl = INFER_BF16_BYTES(C, T), INFER_FLOP(C, T, F1 * D)
     ach = by * B / avg_s / 1e9
@@ -125,7 +130,7 @@ def bench_infer_bf16(dev, B, C, T, F1, D, steps, warmup):
         "value": round(B * steps / dt, 1), "unit": "trials/s", "batch": B, "steps": steps,
         "dtype": "bf16 operands, fp32 accumulation", "finite": bool(torch.isfinite(out).all()),
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None, "kernel": "k_infer_bf16",
+                     "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": "k_infer_bf16",
                      "avg_us": round(avg_s * 1e6, 2), "alg_bytes_per_launch": by * B,
                      "alg_tflops": round(fl * B / avg_s / 1e12, 2)},
     }
