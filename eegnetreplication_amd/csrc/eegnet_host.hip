@@ -216,7 +216,8 @@ static void set_attrs_shape() {
 static void ensure_attrs() {
     if (g_attr_done) return;
     for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
-                          (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>})
+                          (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>,
+                          (const void*)k_infer_bf16<8, true>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 0, 0, 0>();
     set_attrs_shape<64, 0, 0, 0>();
@@ -359,6 +360,14 @@ static int make_geo_bf16(const eegnet_dims* d, GeoI* g) {
     return 0;
 }
 
+// every shape-derived field equal (B, eps and the debug pointer are runtime in every instantiation)
+static bool same_geo_bf16(GeoI a, GeoI b) {
+    a.B = b.B = 0;
+    a.eps = b.eps = 0.f;
+    a.dbg = b.dbg = nullptr;
+    return memcmp(&a, &b, sizeof(GeoI)) == 0;
+}
+
 static int check_ptrs(const void* a, const char* na, const void* b = (const void*)1, const char* nb = "") {
     if (!a) return fail(EEGNET_EINVAL, "%s is NULL", na);
     if (!b) return fail(EEGNET_EINVAL, "%s is NULL", nb);
@@ -462,6 +471,11 @@ int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(std::min(g.B, device_cus())), blk(NTI);
     PROF(KID_INFER_BF16);
+    if (same_geo_bf16(g, kGeoCfg5)) {
+        hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
+        LAUNCH_CHECK("k_infer_bf16(cfg5)");
+        return 0;
+    }
     switch (g.PFU) {
         case 0: hipLaunchKernelGGL(k_infer_bf16<0>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
         case 1: hipLaunchKernelGGL(k_infer_bf16<1>, grid, blk, g.lds, s, g, params, bn_buffers, x, logits); break;
