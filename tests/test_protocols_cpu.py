@@ -61,3 +61,24 @@ def test_report_schema(tmp_path):
     assert r["model_parameters"]["total_folds"] == 90
     assert r["per_subject_results"][8]["performance_rank"] == 1
     assert (tmp_path / "latest_cross_subject_report.json").exists()
+
+
+def test_fold_batch_dispatch_chunks_units(monkeypatch):
+    """train._run_units: fold_batch <= 1 runs units one by one through _run_fold (the
+    reference-shaped train()/evaluate_model() loop); fold_batch = k hands chunks of k units, in
+    order, to _run_folds (FoldBatch).  Results come back in unit order either way."""
+    import importlib
+    T_ = importlib.import_module("eegnetreplication_amd.train")
+    calls = []
+    monkeypatch.setattr(T_, "_run_fold", lambda *a: calls.append(("one", a[7])) or {"seed": a[7]})
+    monkeypatch.setattr(T_, "_run_folds",
+                        lambda specs, e, d: calls.append(("batch", [s[6] for s in specs]))
+                        or [{"seed": s[6]} for s in specs])
+    specs = [(None, None, None, None, None, 0.5, 100 + i) for i in range(7)]
+    out = T_._run_units(specs, 3, "cuda", 0)
+    assert [r["seed"] for r in out] == list(range(100, 107))
+    assert calls == [("one", 100 + i) for i in range(7)]
+    calls.clear()
+    out = T_._run_units(specs, 3, "cuda", 3)
+    assert [r["seed"] for r in out] == list(range(100, 107))
+    assert calls == [("batch", [100, 101, 102]), ("batch", [103, 104, 105]), ("batch", [106])]
