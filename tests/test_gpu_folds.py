@@ -162,3 +162,26 @@ def test_protocol_fold_batch_matches_one_at_a_time():
         assert abs(a["val_loss"] - b["val_loss"]) <= 1e-5 * abs(b["val_loss"]), k
         for n in b["state"]:
             assert torch.equal(a["state"][n], b["state"][n]), f"unit {k}: {n} differs"
+
+
+@pytest.mark.parametrize("sizes", [[64, 30, 128], [1, 65]])
+def test_graph_fold_edge_sizes(sizes):
+    """Edge fold sizes: exactly one batch, a fold smaller than one batch, an exact multiple of 64,
+    a single trial, and 64 + 1 (a one-trial last batch).  Graph replays must match eager runs."""
+    from eegnetreplication_amd import FoldBatch
+    dev = _dev()
+    seeds = [70 + i for i in range(len(sizes))]
+    data = [_data(n, 300 + i, dev) for i, n in enumerate(sizes)]
+    models = _models(len(sizes), 0.5, dev)
+    twins = [_clone(m, 0.5, dev) for m in models]
+    eager, graph = FoldBatch(models, seeds), FoldBatch(twins, seeds, graphs=True)
+    ge = [torch.Generator().manual_seed(s) for s in seeds]
+    gg = [torch.Generator().manual_seed(s) for s in seeds]
+    for _ in range(2):
+        se, sg = eager.epoch(data, 64, ge), graph.epoch(data, 64, gg)
+        torch.cuda.synchronize()
+        for k in range(len(sizes)):
+            assert torch.equal(se[k], sg[k])
+            for a, b in zip(_state(eager, k), _state(graph, k)):
+                assert torch.equal(a, b)
+            assert np.isfinite(float(sg[k]))
