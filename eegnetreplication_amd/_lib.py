@@ -101,8 +101,16 @@ def workspace_bytes(d: Dims) -> int:
     return int(out.value)
 
 
-def profile_enable(on: bool = True):
-    check(load().eegnet_profile_enable(1 if on else 0), "eegnet_profile_enable")
+KERNEL_IDS = ("k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e", "k_adam", "k_infer",
+              "memset_tickets", "k_infer_bf16")
+
+
+def profile_enable(on: bool = True, kernels=None):
+    """Bracket launches with hipEvents: every kernel (``kernels=None``) or only the named ones."""
+    mask = 0
+    if on:
+        mask = -1 if kernels is None else sum(1 << KERNEL_IDS.index(k) for k in kernels)
+    check(load().eegnet_profile_enable(mask), "eegnet_profile_enable")
 
 
 def profile_collect() -> dict:

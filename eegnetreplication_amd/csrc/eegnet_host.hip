@@ -174,7 +174,7 @@ enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
                                               "k_adam", "k_infer", "memset_tickets", "k_infer_bf16"};
 struct ProfRec { int kid; hipEvent_t a, b; };
-struct ProfState { bool on = false; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
+struct ProfState { unsigned mask = 0; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
 
 static hipEvent_t prof_event() {
@@ -186,7 +186,7 @@ static hipEvent_t prof_event() {
 struct ProfScope {
     int kid; hipStream_t s; hipEvent_t a = nullptr;
     ProfScope(int k, hipStream_t st) : kid(k), s(st) {
-        if (g_prof.on) { a = prof_event(); hipEventRecord(a, s); }
+        if ((g_prof.mask >> k) & 1u) { a = prof_event(); hipEventRecord(a, s); }
     }
     ~ProfScope() {
         if (a) { hipEvent_t b = prof_event(); hipEventRecord(b, s); g_prof.recs.push_back({kid, a, b}); }
@@ -570,7 +570,7 @@ int eegnet_trace_enable(void* buf) {
 size_t eegnet_trace_bytes(void) { return (size_t)8 * TR_MAXWG * TR_SLOTS * sizeof(unsigned long long); }
 
 int eegnet_profile_enable(int on) {
-    g_prof.on = on != 0;
+    g_prof.mask = (unsigned)on;
     return 0;
 }
 

@@ -126,10 +126,14 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
                       float eps, float* loss, float* logits, void* ws, void* stream, int flags,
                       int64_t* num_batches_tracked);
 
-/* Optional per-kernel device timing for benchmarks: while enabled, every kernel this thread
- * launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect synchronises
- * them and reports, per kernel name (32-byte slots in `names`), launch count and summed device ms;
- * it returns the number of kernels in *n_out.  Not for use under hipGraph capture. */
+/* Optional per-kernel device timing for benchmarks: `on` is a bitmask of kernel ids (bit i = the
+ * i-th name eegnet_profile_collect reports: k_pass_a, k_pass_b, k_pass_c, k_pass_d, k_pass_e,
+ * k_adam, k_infer, memset_tickets, k_infer_bf16; -1 = all, 0 = off).  Every selected kernel this
+ * thread launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect
+ * synchronises them and reports, per kernel name (32-byte slots in `names`), launch count and
+ * summed device ms; it returns the number of kernels in *n_out.  Not for use under hipGraph
+ * capture.  Each bracketed launch costs a few microseconds of stream time, so a benchmark's timed
+ * region should select only the kernel it prices. */
 int eegnet_profile_enable(int on);
 int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, int* n_out);
 
