@@ -54,3 +54,15 @@ def test_shape_param_layout_matches_library():
     for C, T, F1, D in [(22, 256, 8, 2), (22, 257, 8, 2), (64, 512, 16, 4), (8, 64, 8, 2)]:
         s = Shape(C=C, T=T, F1=F1, D=D)
         assert s.n_params() == _lib.param_count(s.dims(4))
+
+
+def test_flag_and_kernel_id_constants_match_header():
+    """The Python side's flag values and profiling kernel ids are the ones include/eegnet_abi.h
+    documents (EEGNET_NO_CLAMP, EEGNET_KEY_FROM_STEP; eegnet_profile_enable's bit order)."""
+    from eegnetreplication_amd import _lib, ops
+    txt = open(os.path.join(ROOT, "include", "eegnet_abi.h")).read()
+    flags = dict((k, int(v)) for k, v in re.findall(r"(EEGNET_[A-Z_]+)\s*=\s*(\d+)", txt))
+    assert flags["EEGNET_NO_CLAMP"] == ops.NO_CLAMP
+    assert flags["EEGNET_KEY_FROM_STEP"] == ops.KEY_FROM_STEP
+    doc = re.search(r"i-th name eegnet_profile_collect reports:(.*?);", txt, re.S).group(1)
+    assert [n.strip(" *\n") for n in doc.replace("\n", " ").split(",")] == list(_lib.KERNEL_IDS)
