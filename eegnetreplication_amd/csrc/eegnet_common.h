@@ -515,28 +515,6 @@ __device__ __forceinline__ void spatial_mfma_l(const float* Xs, const float* awl
     }
 }
 
-// Lag correlation on the matrix cores.  sum_t a[t] b[t+k-P] (k < K1) = sum_i M[i][i+k] with the
-// row-block matrix M[i][m] = sum_j a[16j+i] b[16j+m-P], m < 16*NTQ, accumulated in NTQ 16x16x4 f32
-// tiles (exact f32 fmaf chains).  Lane l: A[i = l&15][j = 4s + (l>>4)], B[j][m = 16nt + (l&15)];
-// D[4(l>>4)+r][16nt + (l&15)].  a: LDS row at t = 0, zero for t in [T, 16 NJ); b: LDS row at t = 0
-// with >= P zeros on the left; reads of b at t >= T are masked to zero.
-template <int NTQ>
-__device__ __forceinline__ void lagcorr_mfma(const float* a, const float* b, int T, int NJ, int P,
-                                             floatx4 (&acc)[NTQ], int lane) {
-    const int li = lane & 15, lk = lane >> 4;
-    for (int s = 0; 4 * s < NJ; ++s) {
-        const int j = 4 * s + lk;
-        const bool jon = j < NJ;
-        const float av = jon ? a[16 * j + li] : 0.f;
-#pragma unroll
-        for (int nt = 0; nt < NTQ; ++nt) {
-            const int tb = 16 * j + 16 * nt + li - P;
-            const float bv = (jon && tb < T) ? b[tb] : 0.f;
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[nt], 0, 0, 0);
-        }
-    }
-}
-
 // Static shape of a kernel instantiation: CC/TT/FF = 0 means "runtime value from Geo".  The
 // specialised shapes are EEGNet-8,2 (F2 = 16, D = 2); PF = x prefetch floats per thread of an
 // NT_-thread workgroup.

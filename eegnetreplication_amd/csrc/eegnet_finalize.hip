@@ -321,8 +321,11 @@ __device__ void fin4(const Geo& g, const float* prm, const double* sums, const F
 
 // one torch.optim.Adam element update (weight_decay=0, amsgrad=False): torch/optim/adam.py
 // :457,476,531-547 (single-tensor path)
+// Contraction off: the fused (fin5) and standalone (k_adam) instances must round identically, so
+// the data-parallel path is bit-identical to the fused single-device step.
 __device__ __forceinline__ void adam_elem(float* p, float g, float* m, float* v, float b1, float b2,
                                           float step_size, float bc2s, float eps) {
+#pragma clang fp contract(off)
     const float mi = *m + (1.f - b1) * (g - *m);
     const float vi = b2 * *v + (1.f - b2) * g * g;
     *m = mi; *v = vi;

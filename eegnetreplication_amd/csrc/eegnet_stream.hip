@@ -634,20 +634,16 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             wave_lds_fence();                              // dy rows complete; s rows consumed
             // this trial's x operand of the dws GEMM, issued here so the FIR^T covers its latency
             // (the FIR^T holds fewer live registers than the forward FIR + lag correlation)
-        if constexpr (XDMA) {
-            const int c = ct * 16 + li;
-            const float* xr = x + ((size_t)b * C + (c < C ? c : 0)) * T + 4 * lk;
+            if constexpr (XDMA) {
+                const int c = ct * 16 + li;
+                const float* xr = x + ((size_t)b * C + (c < C ? c : 0)) * T + 4 * lk;
 #pragma unroll
-            for (int j = 0; j < NKGW; ++j) {
-                const int kg = kg0 + j;
-#ifdef EXP_NOXG
-                const floatx4 v = (floatx4){0.f, 0.f, 0.f, 0.f};
-#else
-                const floatx4 v = *reinterpret_cast<const floatx4*>(xr + 16 * min(kg, NT16 - 1));
-#endif
-                xg[j] = (gemm_on && kg < kg1 && c < C) ? v : (floatx4){0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < NKGW; ++j) {
+                    const int kg = kg0 + j;
+                    const floatx4 v = *reinterpret_cast<const floatx4*>(xr + 16 * min(kg, NT16 - 1));
+                    xg[j] = (gemm_on && kg < kg1 && c < C) ? v : (floatx4){0.f, 0.f, 0.f, 0.f};
+                }
             }
-        }
             // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
             if (oh < F2) {
                 const float* dyr = Dys + oh * RS;
@@ -670,27 +666,13 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             }
         }
         TRACE_PH(g, 4, 2, tph_);
-        // the next trial's dp2 is fetched here, its x after the GEMM: their registers must not be
+        // the next trial's dp2 is fetched here (register staging only): its registers must not be
         // live across the FIR / FIR^T phase (the kernel's register peak, 128 VGPRs at 4 waves/SIMD);
         // the other workgroup on the CU covers the exposed latency
         // (unconditional loads at clamped addresses: a guarded load compiles to a branch and a wait)
         if (!DPDMA && bn < b1) {
 #pragma unroll
             for (int j = 0; j < NDP; ++j) pdp[j] = dp2g[(size_t)bn * ndp + min(tid + NTB * j, ndp - 1)];
-        }
-        if constexpr (XDMA) {
-            const int c = ct * 16 + li;
-            const float* xr = x + ((size_t)b * C + (c < C ? c : 0)) * T + 4 * lk;
-#pragma unroll
-            for (int j = NKGW; j < NKGW; ++j) {
-                const int kg = kg0 + j;
-#ifdef EXP_NOXG
-                const floatx4 v = (floatx4){0.f, 0.f, 0.f, 0.f};
-#else
-                const floatx4 v = *reinterpret_cast<const floatx4*>(xr + 16 * min(kg, NT16 - 1));
-#endif
-                xg[j] = (gemm_on && kg < kg1 && c < C) ? v : (floatx4){0.f, 0.f, 0.f, 0.f};
-            }
         }
         TRACE_PH(g, 4, 6, tph_);
         __syncthreads();                                   // e rows complete

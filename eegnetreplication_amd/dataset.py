@@ -2,12 +2,13 @@
 
 * ``BCICI2ADataset`` -- the reference's Dataset type (dataset.py:30-43): ``X[n,C,T]`` float64,
   ``y[n]`` int, ``__getitem__ -> (X[i], int(y[i]))``.
-* ``build_dataset_from_preprocessed(subject, mode)`` -- same call as the reference
-  (dataset.py:239-281).  The reference epochs MNE/braindecode-preprocessed GDF recordings; those
-  libraries and the BCI IV-2a files are not available offline, so this build loads
-  ``data/processed/A0{subject}{T|E}.npz`` (arrays ``X``, ``y``) when present and otherwise generates
-  a seeded synthetic motor-imagery-like session with the real shape: 288 trials x 22 channels x
-  257 samples (128 Hz, 0.5-2.5 s), 4 balanced classes.
+* ``build_dataset_from_preprocessed(src, subject, mode)`` -- same call and error behaviour as the
+  reference (dataset.py:239-281).  The reference epochs MNE/braindecode-preprocessed GDF
+  recordings; those libraries and the BCI IV-2a files are not available offline, so
+  this build loads ``data/processed/A0{subject}{T|E}.npz`` (arrays ``X``, ``y``) and raises
+  ``ValueError`` when a file is missing.  Only with ``EEGNET_SYNTHETIC=1`` (CLI ``--synthetic``)
+  does it generate a seeded synthetic motor-imagery-like session instead, with the real shape:
+  288 trials x 22 channels x 257 samples (128 Hz, 0.5-2.5 s), 4 balanced classes.
 * ``DeviceLoader`` -- a device-resident replacement for ``DataLoader(batch_size, shuffle)``: the
   whole split is cast to fp32 and moved to HBM once; batches are index_select views, so the hot
   loop has no per-batch host->device copy (the reference copies every batch, model.py:138).
@@ -15,11 +16,14 @@
 
 from __future__ import annotations
 
+import logging
 import os
 from dataclasses import dataclass
 
 import numpy as np
 import torch
+
+logger = logging.getLogger("eegnet_repl")
 
 N_CHANNELS = 22
 N_SAMPLES = 257
@@ -91,15 +95,61 @@ def data_dir() -> str:
     return os.environ.get("EEGNET_DATA_DIR", os.path.join(os.getcwd(), "data", "processed"))
 
 
-def build_dataset_from_preprocessed(subject: int, mode: str = "Train") -> BCICI2ADataset:
-    """dataset.py:239-281 call signature.  Real epoched data from ``A0{s}{T|E}.npz`` if present
-    (X [288,22,257], y [288]), else the seeded synthetic session."""
-    tag = "T" if mode == "Train" else "E"
-    path = os.path.join(data_dir(), f"A0{subject}{tag}.npz")
+SYNTHETIC_ENV = "EEGNET_SYNTHETIC"
+
+
+def synthetic_enabled() -> bool:
+    """Synthetic sessions are opt-in: ``EEGNET_SYNTHETIC=1`` (or the train CLI's ``--synthetic``)."""
+    return os.environ.get(SYNTHETIC_ENV, "0").lower() not in ("", "0", "false", "no")
+
+
+def _load_session(subject: int, mode: str, synthetic: bool) -> BCICI2ADataset:
+    tag = mode[0]                                  # 'T' (Train) / 'E' (Eval), dataset.py:262
+    path = os.path.join(data_dir(), f"A0{int(subject)}{tag}.npz")
     if os.path.exists(path):
         z = np.load(path, allow_pickle=False)
         return BCICI2ADataset(np.asarray(z["X"], dtype=np.float64), np.asarray(z["y"], dtype=np.int64))
-    return synthetic_session(subject, mode)
+    if synthetic:
+        logger.warning(f"{path} not found: using the seeded SYNTHETIC session for subject {subject} "
+                       f"({mode}) -- results are not BCI IV-2a results")
+        return synthetic_session(int(subject), mode)
+    raise ValueError(f"No preprocessed files found in {data_dir()} for subject {subject} ({path}); "
+                     f"set {SYNTHETIC_ENV}=1 (CLI: --synthetic) to train on seeded synthetic sessions")
+
+
+def build_dataset_from_preprocessed(src="kaggle", subject="all", mode="Train",
+                                    synthetic: bool | None = None) -> BCICI2ADataset:
+    """dataset.py:239-281 call signature and error behaviour.
+
+    Loads the epoched session ``data/processed/A0{subject}{T|E}.npz`` (arrays ``X [288,22,257]``,
+    ``y [288]``; the reference's MNE/braindecode epoching is out of scope).
+    ``subject='all'`` concatenates subjects 1-9 as the reference globs every file.  A missing file
+    raises ``ValueError`` as the reference does (dataset.py:266-267) unless synthetic sessions are
+    enabled (``synthetic=True`` or ``EEGNET_SYNTHETIC=1``), which logs a warning per session.
+    ``src`` must be 'kaggle' or 'moabb' (dataset.py:252-257); both read the same directory here."""
+    if src not in ("kaggle", "moabb"):
+        raise ValueError(f"Unknown source: {src}")
+    if mode not in ("Train", "Eval"):
+        raise ValueError(f"mode must be 'Train' or 'Eval' (got {mode!r})")
+    syn = synthetic_enabled() if synthetic is None else bool(synthetic)
+    subjects = range(1, 10) if subject == "all" else [int(subject)]
+    parts = [_load_session(s, mode, syn) for s in subjects]
+    if len(parts) == 1:
+        return parts[0]
+    return BCICI2ADataset(np.concatenate([p.X for p in parts]), np.concatenate([p.y for p in parts]))
+
+
+def epoch_permutation(n: int, generator=None) -> torch.Tensor:
+    """The trial order ``DataLoader(ds, batch_size, shuffle=True, generator=g)`` produces for one
+    epoch (train.py:87), consuming ``g`` exactly as torch does: the iterator draws a base seed
+    (``_BaseDataLoaderIter``: ``random_(generator=g)``), then ``RandomSampler`` draws
+    ``randperm(n, g)`` and, at exhaustion, one more ``randperm(n, g)`` for the empty remainder."""
+    if generator is None:
+        return torch.randperm(n)
+    torch.empty((), dtype=torch.int64).random_(generator=generator)
+    perm = torch.randperm(n, generator=generator)
+    torch.randperm(n, generator=generator)
+    return perm
 
 
 class DeviceLoader:
@@ -118,7 +168,7 @@ class DeviceLoader:
     def __iter__(self):
         n = len(self.y)
         if self.shuffle:
-            idx = torch.randperm(n, generator=self.generator).to(self.X.device)
+            idx = epoch_permutation(n, self.generator).to(self.X.device)
             for s in range(0, n, self.batch_size):
                 j = idx[s:s + self.batch_size]
                 yield self.X.index_select(0, j), self.y.index_select(0, j)

@@ -5,9 +5,10 @@ Two shapes of parallelism, one process per GPU (torch.distributed; backend "nccl
 * data parallel (cfg4): every rank runs the fused HIP step on its own slice of the global batch,
   the flat fp32 gradient (1,716 floats = 6.9 KB for EEGNet-8,2) is summed with ONE all-reduce per
   step, averaged, then clamped (model.py:44/84 hooks AFTER the reduction, so the clamp sees the
-  global-batch gradient) and Adam runs replicated.  BatchNorm uses per-rank batch
-  statistics (the DDP default).  The message is latency-bound (~7 KB), so there is exactly one
-  collective per step and nothing to bucket.
+  global-batch gradient) and Adam runs replicated.  BatchNorm normalises with per-rank
+  batch statistics and broadcasts rank 0's running statistics each step (DDP's defaults).  The
+  gradient message is latency-bound (~7 KB), so there is exactly one gradient collective per step
+  and nothing to bucket.
 * fold sharding (cfg3): independent cross-/within-subject folds are dealt to ranks by
   longest-processing-time order with no communication on the data path; results are merged on the
   host (``gather_results``).
@@ -55,23 +56,32 @@ def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
 class DataParallelTrainer:
     """Fused HIP train step + one RCCL gradient all-reduce per step (cfg4).
 
-    Per step: local gradients (HIP, clamps deferred) -> all-reduce mean -> model.py:44/84 clamps
-    -> Adam, replicated on every rank.  The three stages are methods so the orchestration can be
-    exercised on CPU (gloo) with a stand-in local step.
+    Per step (``step``): [buffer broadcast] -> local gradients (HIP, clamps deferred) -> all-reduce
+    mean -> model.py:44/84 clamps -> Adam, replicated on every rank.  BatchNorm normalises with
+    per-rank batch statistics; the running statistics follow DDP's default
+    ``broadcast_buffers=True``: rank 0's running_mean/var and num_batches_tracked are broadcast to
+    every rank before each local forward, so every rank evaluates and checkpoints rank 0's buffers.
+    The stages are methods so the orchestration can be exercised on CPU (gloo) with stand-ins for
+    the device kernels.
     """
 
-    def __init__(self, model: EEGNet, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, group=None):
+    def __init__(self, model: EEGNet, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, group=None,
+                 broadcast_buffers=True):
         self.model = model
         self.lr, self.betas, self.eps = lr, betas, eps
         self.group = group
+        self.broadcast_buffers = broadcast_buffers
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         flat = model.flat_parameters()
         if self.world > 1:   # identical start on every rank
-            dist.broadcast(flat, 0, group=group)
+            dist.broadcast(flat, self._src(0), group=group)
         self._init_state(flat)
         self._ws = {}
         self._step = 0
+
+    def _src(self, r):
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
 
     def _init_state(self, flat):
         self.adam = FusedAdamState(self.model)
@@ -85,12 +95,22 @@ class DataParallelTrainer:
         return ws
 
     # -- stages ------------------------------------------------------------------------------
+    def sync_buffers(self):
+        """DDP broadcast_buffers: rank 0's BN running statistics and counters to every rank."""
+        if self.world > 1:
+            dist.broadcast(self.model.flat_bn_buffers(), self._src(0), group=self.group)
+            dist.broadcast(self.model.flat_num_batches_tracked(), self._src(0), group=self.group)
+
     def local_grads(self, x, y, seed, offset):
         m = self.model
         ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
                        self.adam.grads, None, None, self.workspace(x.shape[0]), self.loss,
                        clamp=False, nbt=m.flat_num_batches_tracked())
         return self.adam.grads
+
+    def reduce(self, grads):
+        """ONE all-reduce (SUM) of the flat gradient, then x 1/world: CE is a batch mean."""
+        return allreduce_mean_(grads, self.group)
 
     def clamp(self, grads):
         ops.clamp_grads(self.model.shape, grads)
@@ -105,8 +125,10 @@ class DataParallelTrainer:
         self._step += 1
         seed = 0x5EED_0000 + self._step
         offset = self._step * self.world + self.rank        # distinct masks on every rank
+        if self.broadcast_buffers:
+            self.sync_buffers()
         grads = self.local_grads(x, y, seed, offset)
-        allreduce_mean_(grads, self.group)
+        self.reduce(grads)
         self.clamp(grads)
         self.update(grads)
         return self.loss

@@ -21,6 +21,7 @@ from __future__ import annotations
 import torch
 
 from . import ops
+from .dataset import epoch_permutation
 from .model import EEGNet, FusedAdamState
 
 
@@ -83,8 +84,8 @@ class FoldBatch:
     def epoch(self, data: list[tuple[torch.Tensor, torch.Tensor]], batch_size: int = 64,
               generators: list[torch.Generator] | None = None) -> list[torch.Tensor]:
         """One training epoch of every fold.  ``data[k] = (X_k [N_k,C,T] fp32, y_k [N_k] int64)``,
-        device-resident.  Each fold is shuffled by its own generator (DataLoader(shuffle=True),
-        train.py:87) and cut into batches of ``batch_size`` with a short last batch
+        device-resident.  Each fold is shuffled by its own generator exactly as
+        DataLoader(shuffle=True, generator=g) would (train.py:87; dataset.epoch_permutation) and cut into batches of ``batch_size`` with a short last batch
         (drop_last=False).  Returns per-fold float64 device scalars: the sum of the batch losses
         (the reference's running loss, model.py:150).  Nothing is synchronised."""
         if len(data) != len(self.models):
@@ -95,7 +96,7 @@ class FoldBatch:
             n = X.shape[0]
             nsteps = (n + batch_size - 1) // batch_size
             g = generators[k] if generators is not None else None
-            perm = torch.randperm(n, generator=g) if g is not None else torch.arange(n)
+            perm = epoch_permutation(n, g) if g is not None else torch.arange(n)
             s = self.streams[k]
             s.wait_stream(cur)
             st = self._graph[k]

@@ -138,12 +138,20 @@ def within_subject_units():
     return units
 
 
-def within_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0):
+def _select(units, max_units, world, rank):
+    """This rank's unit indices: all units (or the first ``max_units``, a smoke-test restriction
+    the reference does not have), dealt by LPT over the ranks."""
+    n = len(units) if not max_units else min(int(max_units), len(units))
+    return D.lpt_assign([1.0] * n, world)[rank] if world > 1 else list(range(n))
+
+
+def within_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0, max_units=None):
     """train.py:30-148.  Returns (per_subject_test_acc, avg_test_acc, best_model_states).
-    ``fold_batch`` > 1 trains that many of this rank's units together (FoldBatch)."""
+    ``fold_batch`` > 1 trains that many of this rank's units together (FoldBatch).
+    ``max_units`` restricts the run to the first units (subjects with no unit are left out)."""
     rank, world, _ = D.env_rank_world()
     units = within_subject_units()
-    mine = D.lpt_assign([1.0] * len(units), world)[rank] if world > 1 else range(len(units))
+    mine = _select(units, max_units, world, rank)
     cache, local, specs = {}, {}, []
     for u in mine:
         s, f = units[u]
@@ -166,11 +174,15 @@ def within_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0):
     for s in range(1, N_SUBJECTS + 1):
         accs, best_val, best_state = [], 0, None
         for f in range(4):
+            if units.index((s, f)) not in res:
+                continue
             r = res[units.index((s, f))]
             logger.info(f"Subject {s} fold {f + 1}: val {r['val_acc']:.2f}% test {r['test_acc']:.2f}%")
             accs.append(r["test_acc"])
             if r["val_acc"] > best_val:
                 best_val, best_state = r["val_acc"], r["state"]
+        if not accs:
+            continue
         per_subject.append(sum(accs) / len(accs))
         states.append(best_state)
     avg = sum(per_subject) / len(per_subject)
@@ -189,12 +201,13 @@ def cross_subject_units():
     return units
 
 
-def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0):
+def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0, max_units=None):
     """train.py:151-291.  Returns (best_model_state, per_subject_test_acc, avg_test_acc).
-    ``fold_batch`` > 1 trains that many of this rank's folds together (FoldBatch)."""
+    ``fold_batch`` > 1 trains that many of this rank's folds together (FoldBatch).
+    ``max_units`` restricts the run to the first folds (subjects with no fold are left out)."""
     rank, world, _ = D.env_rank_world()
     units = cross_subject_units()
-    mine = D.lpt_assign([1.0] * len(units), world)[rank] if world > 1 else range(len(units))
+    mine = _select(units, max_units, world, rank)
     sessions = {}
 
     def sess(s, mode):
@@ -220,14 +233,15 @@ def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0):
     for s in range(1, N_SUBJECTS + 1):
         accs = []
         for u, unit in enumerate(units):
-            if unit[0] != s:
+            if unit[0] != s or u not in res:
                 continue
             r = res[u]
             accs.append(r["test_acc"])
             all_acc.append(r["test_acc"])
             if r["val_loss"] < best_loss:
                 best_loss, best_state = r["val_loss"], r["state"]
-        per_subject.append(sum(accs) / len(accs))
+        if accs:
+            per_subject.append(sum(accs) / len(accs))
     avg = sum(all_acc) / len(all_acc)
     se = float(np.std(all_acc) / np.sqrt(len(all_acc)))
     logger.info(f"Overall Average Test Accuracy: {avg:.2f}% +- {se:.2f}%")
@@ -253,6 +267,14 @@ def _summary(per_subject, avg):
             "q2_median": round(float(np.percentile(per_subject, 50)), 2),
             "q3": round(float(np.percentile(per_subject, 75)), 2)},
     }
+
+
+def _mark_data_source(report):
+    """Reports trained on seeded synthetic sessions say so (the reference schema is unchanged for
+    real data)."""
+    from .dataset import synthetic_enabled
+    if synthetic_enabled():
+        report["data_source"] = "synthetic SMR-like sessions (EEGNET_SYNTHETIC=1), not BCI IV-2a"
 
 
 def _write_report(report, prefix, out_dir):
@@ -287,6 +309,7 @@ def generate_ws_report(per_subject_test_acc, avg, states, out_dir="reports"):
                        "loss_function": "CrossEntropyLoss", "saved_models_count": len(states)},
         "summary_statistics": _summary(per_subject_test_acc, avg),
     }
+    _mark_data_source(report)
     return _write_report(report, "within_subject", out_dir)
 
 
@@ -310,6 +333,7 @@ def generate_cs_report(best_state, per_subject_test_acc, avg, out_dir="reports")
                        "loss_function": "CrossEntropyLoss", "saved_model": "cross_subject_best_model.pth"},
         "summary_statistics": _summary(per_subject_test_acc, avg),
     }
+    _mark_data_source(report)
     return _write_report(report, "cross_subject", out_dir)
 
 
@@ -323,7 +347,14 @@ def main(argv=None) -> None:
     ap.add_argument("--out", type=str, default=".", help="directory for models/ and reports/")
     ap.add_argument("--fold-batch", type=int, default=16,
                     help="train this many folds together on one GPU (FoldBatch); 0/1: one at a time")
+    ap.add_argument("--max-units", type=int, default=0,
+                    help="smoke runs: only the first N folds of the protocol (0 = all)")
+    ap.add_argument("--synthetic", action="store_true",
+                    help="train on seeded synthetic sessions when data/processed/*.npz is absent "
+                         "(same as EEGNET_SYNTHETIC=1); the reports record it")
     args = ap.parse_args(argv)
+    if args.synthetic:
+        os.environ["EEGNET_SYNTHETIC"] = "1"
     logging.basicConfig(level=logging.INFO,
                         format="%(asctime)s - %(filename)s - %(funcName)s - %(levelname)s - %(message)s",
                         handlers=[logging.FileHandler("app.log"), logging.StreamHandler()])
@@ -333,15 +364,17 @@ def main(argv=None) -> None:
     models_dir = os.path.join(args.out, "models")
     reports_dir = os.path.join(args.out, "reports")
     if args.trainingType == "Within-Subject":
-        per_subject, avg, states = within_subject_training(args.epochs, args.seed, device, args.fold_batch)
+        per_subject, avg, states = within_subject_training(args.epochs, args.seed, device, args.fold_batch,
+                                                           args.max_units)
         if rank == 0:
             os.makedirs(models_dir, exist_ok=True)
-            for s, st in enumerate(states, 1):
+            for s, st in enumerate(states, 1):        # train.py:136-139 (max_units keeps 1..k)
                 torch.save(st, os.path.join(models_dir, f"subject_{s:02d}_best_model.pth"))
             if args.generateReport:
                 generate_ws_report(per_subject, avg, states, reports_dir)
     else:
-        best, per_subject, avg = cross_subject_training(args.epochs, args.seed, device, args.fold_batch)
+        best, per_subject, avg = cross_subject_training(args.epochs, args.seed, device, args.fold_batch,
+                                                        args.max_units)
         if rank == 0:
             os.makedirs(models_dir, exist_ok=True)
             torch.save(best, os.path.join(models_dir, "cross_subject_best_model.pth"))

@@ -22,7 +22,9 @@
  *       classifier.weight[4,F2*(T/32)] classifier.bias[4]          (F2 = F1*D)
  *     (1,716 floats for EEGNet-8,2 at C=22, T=256).  `grads` has the same layout.
  *   - `bn_buffers` is one flat fp32 buffer: running_mean/running_var of temporal.1 [F1,F1],
- *     aggregation.0 [F2,F2], block_2.2 [F2,F2] (num_batches_tracked stays on the host).
+ *     aggregation.0 [F2,F2], block_2.2 [F2,F2].  The three num_batches_tracked counters are an
+ *     optional separate int64[3] device buffer (the last argument of eegnet_forward_train and
+ *     eegnet_train_step; NULL = not tracked), incremented in-kernel once per train-mode forward.
  *   - x is [B,C,T] fp32 row-major; labels int64 [B] in [0,4); logits fp32 [B,4].
  *   - Dropout keep-masks: uint8 [B,F2,T/4] and [B,F2,T/128] (1 = keep), nullable.  NULL means the
  *     on-device counter-based generator keyed by (seed, offset): the same (seed, offset) always

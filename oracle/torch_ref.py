@@ -27,15 +27,17 @@ from .numpy_ref import BN_EPS, BN_MOMENTUM, PARAM_NAMES, BN_PREFIXES, same_pad
 class TorchRefEEGNet:
     """Holds fp32 leaf tensors named like the reference state_dict; forward == model.py:91-99."""
 
-    def __init__(self, state: dict, p: float = 0.5, device="cpu"):
+    def __init__(self, state: dict, p: float = 0.5, device="cpu", dtype=torch.float32):
+        """``dtype=torch.float64`` turns the same ATen layer stack into a float64 oracle (used by
+        the GPU tests at sizes the numpy oracle is too slow for)."""
         self.p = p
-        self.params = {k: torch.as_tensor(state[k], dtype=torch.float32, device=device)
+        self.params = {k: torch.as_tensor(state[k], dtype=dtype, device=device)
                        .clone().requires_grad_(True) for k in PARAM_NAMES}
         self.buffers = {}
         for pre in BN_PREFIXES:
             for suf in ("running_mean", "running_var"):
                 self.buffers[f"{pre}.{suf}"] = torch.as_tensor(
-                    state[f"{pre}.{suf}"], dtype=torch.float32, device=device).clone()
+                    state[f"{pre}.{suf}"], dtype=dtype, device=device).clone()
             self.buffers[f"{pre}.num_batches_tracked"] = torch.as_tensor(
                 state[f"{pre}.num_batches_tracked"], dtype=torch.int64, device=device).clone()
         # model.py:44 and model.py:84 -- clamp the gradient, not the weight

@@ -56,6 +56,39 @@ def test_shape_param_layout_matches_library():
         assert s.n_params() == _lib.param_count(s.dims(4))
 
 
+def _header_param_count(name):
+    txt = open(os.path.join(ROOT, "include", "eegnet_abi.h")).read()
+    m = re.search(r"^\s*(?:int|size_t|const char\*)\s+" + name + r"\s*\((.*?)\);", txt, re.S | re.M)
+    args = m.group(1).strip()
+    return 0 if args in ("", "void") else args.count(",") + 1
+
+
+def test_binding_argument_counts_match_header():
+    """Every ctypes signature has exactly as many arguments as the C prototype (a short argtypes
+    list leaves trailing pointer arguments -- e.g. num_batches_tracked -- undefined)."""
+    from eegnetreplication_amd import _lib
+    for name, (_, args) in _lib._SIGS.items():
+        assert len(args) == _header_param_count(name), name
+
+
+def test_integration_ctypes_example_matches_binding():
+    """The ctypes snippet a maintainer copies from INTEGRATION.md binds eegnet_train_step with the
+    full parameter list (it once omitted num_batches_tracked) and passes every argument."""
+    from eegnetreplication_amd import _lib
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = re.search(r"lib\.eegnet_train_step\.argtypes = \[(.*?)\]\n", txt, re.S)
+    n_decl = m.group(1).count(",") + 1
+    assert n_decl == len(_lib._SIGS["eegnet_train_step"][1]) == _header_param_count("eegnet_train_step")
+    call = re.search(r"rc = lib\.eegnet_train_step\((.*?)\)\s*(?:#.*)?\n(?=if rc)", txt, re.S).group(1)
+    call = re.sub(r"#[^\n]*", "", call)
+    depth, n_args = 0, 1
+    for ch in call:
+        depth += ch == "("
+        depth -= ch == ")"
+        n_args += ch == "," and depth == 0
+    assert n_args == n_decl
+
+
 def test_flag_and_kernel_id_constants_match_header():
     """The Python side's flag values and profiling kernel ids are the ones include/eegnet_abi.h
     documents (EEGNET_NO_CLAMP, EEGNET_KEY_FROM_STEP; eegnet_profile_enable's bit order)."""

@@ -1,6 +1,7 @@
-"""Multi-process orchestration on CPU (gloo, world_size 2): the data-parallel step's
-all-reduce -> clamp -> Adam order, and fold sharding / result gathering.  The HIP local step is
-replaced by the CPU oracle (test-only stand-in); everything else is the product code."""
+"""Multi-process orchestration on CPU (gloo, world_size 2): the product DataParallelTrainer.step
+(buffer broadcast -> local step -> all-reduce mean -> clamp -> Adam), and fold sharding / result
+gathering.  The device stages are stand-ins here (the local step is the float64 oracle); their HIP
+kernels are checked on the GPU in tests/test_gpu_distributed.py."""
 
 from __future__ import annotations
 
@@ -29,37 +30,14 @@ def _flat(d):
                       for k in PARAM_NAMES])
 
 
-def _oracle_local_grads(params, bufs, x, y):
-    from oracle import numpy_ref as nr
-    logits, cache, _ = nr.forward(params, bufs, x, train=True, p=0.0)
-    _, dl = nr.cross_entropy(logits, y)
-    g = nr.backward(cache, dl)
-    # undo the clamp: the DP path defers it until after the all-reduce
-    return g
-
-
-def _clamp_flat(grads, shapes):
-    out, o = [], 0
-    for k, shp in shapes:
-        n = int(np.prod(shp))
-        v = grads[o:o + n]
-        if k == "spatial.weight":
-            v = v.clamp(-1.0, 1.0)
-        elif k == "classifier.weight":
-            v = v.clamp(-0.25, 0.25)
-        out.append(v)
-        o += n
-    return torch.cat(out)
-
-
 def _shapes():
     g = Golden("G6")
     return [(k, np.asarray(g.init_params()[k]).shape) for k in PARAM_NAMES]
 
 
 def _rank_grads(rank, world):
-    """Unclamped local gradients of rank's half of the clamp-active G6 batch (CPU oracle as the
-    stand-in for the HIP local step; per-rank BN statistics as in DataParallelTrainer)."""
+    """Unclamped local gradients of rank's slice of the clamp-active G6 batch (the float64 oracle
+    stands in for the HIP local step; per-rank BN statistics as in DataParallelTrainer)."""
     from oracle import numpy_ref as nr
     g = Golden("G6")
     params, bufs = g.init_params(), g.init_buffers()
@@ -67,31 +45,52 @@ def _rank_grads(rank, world):
     xs, ys = g.x[rank * half:(rank + 1) * half], g.y[rank * half:(rank + 1) * half]
     logits, cache, _ = nr.forward(params, bufs, xs, train=True, p=0.0)
     _, dl = nr.cross_entropy(logits, ys)
-    grads = nr.backward(cache, dl * 1000.0)
-    dz = dl * 1000.0
-    grads["classifier.weight"] = dz.T @ cache["h"]           # undo the oracle's clamp
-    ws = params["spatial.weight"].reshape(16, 22).astype(np.float64)
-    del ws
-    return _flat(grads)
+    return _flat(nr.backward(cache, dl * g.meta["loss_scale"], clamp=False))
 
 
 def _worker(rank, world, port, q):
+    """Drives the product DataParallelTrainer.step (buffer broadcast -> local grads -> reduce ->
+    clamp -> update) on CPU/gloo.  Only the device stages are stand-ins: local_grads returns the
+    oracle's unclamped local gradient, clamp / update record what reaches them (the HIP clamp and
+    Adam kernels are checked on the GPU: tests/test_gpu_distributed.py)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from eegnetreplication_amd import EEGNet
     from eegnetreplication_amd import distributed as D
     D.init_process_group("gloo")
-    grads = _rank_grads(rank, world)
-    D.allreduce_mean_(grads)
-    clamped = _clamp_flat(grads, _shapes())
+    torch.manual_seed(100 + rank)                 # different init per rank: the trainer broadcasts
+    model = EEGNet(22, 256, p=0.0)
+    with torch.no_grad():
+        model.flat_bn_buffers().fill_(float(rank + 1))      # rank-specific running statistics
+        model.flat_num_batches_tracked().fill_(10 * (rank + 1))
+    tr = D.DataParallelTrainer(model)
+    calls = []
+
+    def local_grads(x, y, seed, offset):
+        calls.append(("local", seed, offset, model.flat_bn_buffers().clone()))
+        tr.adam.grads = _rank_grads(rank, world).float()
+        return tr.adam.grads
+
+    def clamp(grads):
+        calls.append(("clamp", grads.clone()))
+
+    def update(grads):
+        calls.append(("update", grads.data_ptr() == tr.adam.grads.data_ptr()))
+
+    tr.local_grads, tr.clamp, tr.update = local_grads, clamp, update
+    tr.step(None, None)
+    nbt = model.flat_num_batches_tracked().clone()
     # fold sharding + gather
     assign = D.lpt_assign([5, 1, 4, 2, 3, 9, 7], world)
     local = {u: rank * 100 + u for u in assign[rank]}
     merged = D.gather_results(local)
-    q.put((rank, clamped.numpy(), sorted(merged.items()), assign))
+    q.put((rank, [c[0] for c in calls], calls[0][1:3], calls[0][3].numpy(), calls[1][1].numpy(),
+           calls[2][1], model.flat_parameters().detach().numpy().copy(), nbt.numpy(),
+           sorted(merged.items()), assign))
     dist.destroy_process_group()
 
 
-def test_dp_allreduce_then_clamp_and_fold_sharding():
+def test_dp_trainer_step_order_and_fold_sharding():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -103,17 +102,22 @@ def test_dp_allreduce_then_clamp_and_fold_sharding():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
-    # every rank ends with the same clamped global-mean gradient
-    np.testing.assert_array_equal(res[0][1], res[1][1])
-    # and it is clamp(mean(g_r)) -- the clamp sees the global gradient
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert r[1] == ["local", "clamp", "update"]          # clamp after the reduction, then Adam
+        assert r[5] is True                                   # Adam consumes the reduced buffer
+        np.testing.assert_array_equal(r[3], np.ones_like(r[3]))  # rank 0's BN buffers broadcast first
+        np.testing.assert_array_equal(r[7], [10, 10, 10])
+    # distinct dropout keys per rank, same seed
+    assert res[0][2][0] == res[1][2][0] and res[0][2][1] != res[1][2][1]
+    # identical parameters on every rank after the initial broadcast
+    np.testing.assert_array_equal(res[0][6], res[1][6])
+    # what reaches the clamp is the global-mean gradient (clamp the global gradient)
     g0, g1 = _rank_grads(0, world), _rank_grads(1, world)
-    expected = _clamp_flat((g0 + g1) / 2, _shapes())
-    np.testing.assert_allclose(res[0][1], expected.numpy(), rtol=1e-12, atol=1e-15)
-    cls = slice(sum(int(np.prod(s)) for _, s in _shapes()[:10]), None)
-    assert np.max(np.abs(res[0][1][cls][:-4])) <= 0.25 + 1e-12     # classifier.weight (not .bias)
-    merged = dict(res[0][2])
-    assign = res[0][3]
+    for r in res:
+        np.testing.assert_array_equal(r[4], ((g0.float() + g1.float()) * 0.5).numpy())
+    merged = dict(res[0][8])
+    assign = res[0][9]
     assert sorted(merged) == list(range(7))
     for r in range(world):
         for u in assign[r]:

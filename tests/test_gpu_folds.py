@@ -86,7 +86,8 @@ def test_single_fold_matches_fused_trainer():
     ref = _clone(m, 0.0, dev)
     fb = FoldBatch([m], [1])
     fb.epoch([(X, y)], 64, [torch.Generator().manual_seed(3)])
-    perm = torch.randperm(150, generator=torch.Generator().manual_seed(3)).to(dev)
+    from eegnetreplication_amd.dataset import epoch_permutation
+    perm = epoch_permutation(150, torch.Generator().manual_seed(3)).to(dev)
     tr = FusedTrainer(ref)
     for i in range(0, 150, 64):
         idx = perm[i:i + 64]

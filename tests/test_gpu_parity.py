@@ -122,42 +122,10 @@ def test_fused_trajectory_G7():
                         g.group("final"), steps=g.meta["steps"], rtol=2e-4, atol_frac=2e-4)
 
 
-def test_large_batch_against_torch_fp32():
-    """cfg2 shape (B=4096, 22x256, p=0.5): HIP grads vs the torch fp32 restatement on the same
-    device with the same injected masks (size-independent check at the benchmark size)."""
-    from eegnetreplication_amd import EEGNet
-    from oracle import torch_ref as tr
-    dev = _dev()
-    B, C, T = 4096, 22, 256
-    torch.manual_seed(0)
-    model = EEGNet(C, T, p=0.5).to(dev).train()
-    state = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
-    x_np, y_np = make_inputs(B, C, T, 1234)
-    m2, m3 = make_masks(B, 16, T, 99, 0.5)
-    x, y = torch.from_numpy(x_np).to(dev), torch.from_numpy(y_np).to(dev)
-    model.set_dropout_masks(torch.from_numpy(m2).to(dev), torch.from_numpy(m3).to(dev))
-    logits = model(x)
-    loss = torch.nn.functional.cross_entropy(logits, y)
-    loss.backward()
-    ref = tr.TorchRefEEGNet(state, p=0.5, device=dev)
-    rl = ref(x, (torch.from_numpy(m2).to(dev), torch.from_numpy(m3).to(dev)))
-    rloss = torch.nn.functional.cross_entropy(rl, y)
-    rloss.backward()
-    assert_close(logits.detach().cpu().numpy(), rl.detach().cpu().numpy(), name="logits")
-    assert_grads_close({k: p.grad.cpu().numpy() for k, p in model.named_parameters()},
-                       {k: ref.params[k].grad.cpu().numpy() for k in PARAM_NAMES},
-                       rtol=1e-3, atol_frac=1e-4, prefix="B4096 grad.")
-    # running means of batch-normalised, zero-mean data are ~1e-5 of their unit scale, where the
-    # fp32 reference's own summation error (~1e-7 sqrt(n)) dominates: compare on that scale
-    for k, b in model.named_buffers():
-        if "running_mean" in k:
-            assert_close(b.cpu().numpy(), ref.buffers[k].cpu().numpy(), atol_abs=1e-6, name=k)
-        elif "running_var" in k:
-            assert_close(b.cpu().numpy(), ref.buffers[k].cpu().numpy(), name=k)
-
-
 def test_dropout_generator_properties():
-    """On-device masks: deterministic per (seed, offset), keep rate 1-p, forward/backward agree."""
+    """On-device masks are deterministic per (seed, offset) and change with the offset; with p = 0
+    the key is irrelevant.  (Keep rate, scale, forward/backward agreement and the exact masks are
+    checked against a restatement of the generator in tests/test_gpu_coverage.py.)"""
     from eegnetreplication_amd import EEGNet
     from eegnetreplication_amd import ops
     dev = _dev()

@@ -1,0 +1,183 @@
+"""The reference's own model-test contract (/root/reference/tests/test_model.py:30-185, 236-280),
+restated against the drop-in ``eegnet_repl.model`` (= eegnetreplication_amd.model).
+
+Structure tests construct modules only and run on CPU.  Everything that computes runs with the
+model and tensors on the HIP device (``cuda``): this build has no CPU compute path, so the
+reference's CPU tensors are moved to the device -- otherwise the assertions are the reference's.
+The reference's two "signature" tests call train()/evaluate_model() with Mock objects and swallow
+every exception (test_model.py:188-230); here the signatures are checked with inspect instead.
+"""
+
+from __future__ import annotations
+
+import inspect
+
+import pytest
+import torch
+import torch.nn as nn
+
+from eegnet_repl.model import EEGNet, evaluate_model, train
+
+C, T, NCLS = 22, 256, 4
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+# ---- structure (test_model.py:30-54, 123-185) -----------------------------------------------
+def test_model_initialization_default():
+    model = EEGNet(C=C, T=T)
+    assert isinstance(model, nn.Module) and isinstance(model, EEGNet)
+    for name in ("temporal", "spatial", "aggregation", "block_2", "classifier"):
+        assert hasattr(model, name)
+
+
+def test_model_initialization_custom_params():
+    F1, D, p = 16, 4, 0.25
+    model = EEGNet(C=C, T=T, F1=F1, D=D, p=p)
+    assert model.temporal[0].out_channels == F1
+    assert model.spatial.in_channels == F1
+    assert model.spatial.out_channels == D * F1
+
+
+def test_temporal_conv_properties():
+    conv = EEGNet(C=C, T=T, F1=8).temporal[0]
+    assert conv.kernel_size == (1, 32)
+    assert conv.bias is None
+    assert conv.in_channels == 1 and conv.out_channels == 8
+
+
+def test_spatial_conv_properties():
+    model = EEGNet(C=C, T=T, F1=8, D=2)
+    assert model.spatial.kernel_size == (C, 1)
+    assert model.spatial.groups == 8
+    assert model.spatial.bias is None
+    assert model.spatial.in_channels == 8 and model.spatial.out_channels == 16
+
+
+def test_classifier_properties():
+    model = EEGNet(C=C, T=T, F1=8, D=2)
+    assert model.classifier.out_features == NCLS
+    assert model.classifier.bias is not None
+
+
+def test_dropout_probability():
+    model = EEGNet(C=C, T=T, p=0.3)
+    drops = [m for m in model.modules() if isinstance(m, nn.Dropout)]
+    assert len(drops) == 2
+    assert all(d.p == 0.3 for d in drops)
+
+
+def test_state_dict_keys_and_shapes_match_reference_layout():
+    """the 21 state_dict keys of the reference model, same shapes (checkpoint format)."""
+    sd = EEGNet(C=C, T=T).state_dict()
+    expect = {
+        "temporal.0.weight": (8, 1, 1, 32), "temporal.1.weight": (8,), "temporal.1.bias": (8,),
+        "temporal.1.running_mean": (8,), "temporal.1.running_var": (8,),
+        "temporal.1.num_batches_tracked": (), "spatial.weight": (16, 1, 22, 1),
+        "aggregation.0.weight": (16,), "aggregation.0.bias": (16,),
+        "aggregation.0.running_mean": (16,), "aggregation.0.running_var": (16,),
+        "aggregation.0.num_batches_tracked": (), "block_2.0.weight": (16, 1, 1, 16),
+        "block_2.1.weight": (16, 16, 1, 1), "block_2.2.weight": (16,), "block_2.2.bias": (16,),
+        "block_2.2.running_mean": (16,), "block_2.2.running_var": (16,),
+        "block_2.2.num_batches_tracked": (), "classifier.weight": (4, 128), "classifier.bias": (4,),
+    }
+    assert list(sd) == list(expect)
+    for k, s in expect.items():
+        assert tuple(sd[k].shape) == s, k
+    assert sum(p.numel() for p in EEGNet(C=C, T=T).parameters()) == 1716
+
+
+def test_train_and_evaluate_signatures():
+    """model.py:101 train(model, optimizer, loss_fn, train_loader, val_loader, nepochs=500);
+    model.py:191 evaluate_model(model, test_loader)."""
+    ps = inspect.signature(train).parameters
+    assert list(ps)[:6] == ["model", "optimizer", "loss_fn", "train_loader", "val_loader", "nepochs"]
+    assert ps["nepochs"].default == 500
+    assert list(inspect.signature(evaluate_model).parameters)[:2] == ["model", "test_loader"]
+
+
+def test_cpu_tensors_raise_instead_of_falling_back():
+    model = EEGNet(C=C, T=T)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        model(torch.randn(2, C, T))
+
+
+# ---- computation (test_model.py:56-121, 236-280), on the device ------------------------------
+@pytest.mark.gpu
+def test_forward_pass_shape_and_type():
+    dev = _dev()
+    model = EEGNet(C=C, T=T).to(dev)
+    out = model(torch.randn(16, C, T, device=dev))
+    assert isinstance(out, torch.Tensor)
+    assert out.shape == (16, NCLS) and out.dtype == torch.float32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 8, 16, 32])
+def test_forward_pass_different_batch_sizes(B):
+    dev = _dev()
+    model = EEGNet(C=C, T=T).to(dev)
+    out = model(torch.randn(B, C, T, device=dev))
+    assert out.shape == (B, NCLS)
+    assert torch.isfinite(out).all()
+
+
+@pytest.mark.gpu
+def test_model_gradients():
+    dev = _dev()
+    model = EEGNet(C=C, T=T).to(dev)
+    x = torch.randn(16, C, T, device=dev)
+    target = torch.randint(0, NCLS, (16,), device=dev)
+    nn.CrossEntropyLoss()(model(x), target).backward()
+    for name, param in model.named_parameters():
+        assert param.grad is not None, f"Parameter {name} has no gradient"
+        assert torch.isfinite(param.grad).all(), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Cc,Tt", [(64, 128), (32, 512), (8, 64)])
+def test_model_different_input_sizes(Cc, Tt):
+    dev = _dev()
+    model = EEGNet(C=Cc, T=Tt).to(dev)
+    out = model(torch.randn(4, Cc, Tt, device=dev))
+    assert out.shape == (4, NCLS)
+    model.eval()
+    with torch.no_grad():
+        assert model(torch.randn(4, Cc, Tt, device=dev)).shape == (4, NCLS)
+
+
+@pytest.mark.gpu
+def test_model_training_step():
+    dev = _dev()
+    model = EEGNet(C=22, T=256).to(dev)
+    optimizer = torch.optim.Adam(model.parameters())
+    loss_fn = nn.CrossEntropyLoss()
+    x = torch.randn(8, 22, 256, device=dev)
+    y = torch.randint(0, 4, (8,), device=dev)
+    model.train()
+    before = [p.detach().clone() for p in model.parameters()]
+    optimizer.zero_grad()
+    output = model(x.float())
+    loss = loss_fn(output, y)
+    loss.backward()
+    optimizer.step()
+    assert not torch.isnan(loss) and not torch.isinf(loss)
+    assert output.shape == (8, 4)
+    for p, b in zip(model.parameters(), before):
+        assert torch.isfinite(p).all()
+    assert any(not torch.equal(p, b) for p, b in zip(model.parameters(), before))
+
+
+@pytest.mark.gpu
+def test_model_evaluation_step():
+    dev = _dev()
+    model = EEGNet(C=22, T=256).to(dev)
+    model.eval()
+    with torch.no_grad():
+        output = model(torch.randn(4, 22, 256, device=dev).float())
+    assert output.shape == (4, 4) and isinstance(output, torch.Tensor)
+    assert not torch.any(torch.isnan(output)) and not torch.any(torch.isinf(output))

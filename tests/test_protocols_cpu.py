@@ -28,15 +28,39 @@ def test_cross_subject_fold_permutations():
     assert units[-1][2] == [1, 6, 4, 5, 7] and units[-1][3] == [8, 3, 2]
     for s, k, tr, va in units:
         assert s not in tr + va and len(set(tr + va)) == 8
-    blob = json.dumps([[u[2], u[3]] for u in units]).encode()
-    assert len(hashlib.sha256(blob).hexdigest()) == 64
+    # all 90 folds, pinned by the survey's digest of [subject, repeat (0-based), train, val]
+    # rows serialised with json.dumps (sha256 f35bda7822d73141...)
+    rows = [[s, (k - 1) % 10, tr, va] for s, k, tr, va in units]
+    digest = hashlib.sha256(json.dumps(rows).encode()).hexdigest()
+    assert digest.startswith("f35bda7822d73141"), digest
+
+
+def test_missing_data_raises_unless_synthetic(tmp_path, monkeypatch):
+    """dataset.py:266-267: no preprocessed file -> ValueError.  Synthetic sessions are opt-in."""
+    import pytest
+    from eegnetreplication_amd import dataset as ds
+    monkeypatch.setenv("EEGNET_DATA_DIR", str(tmp_path))
+    monkeypatch.delenv("EEGNET_SYNTHETIC", raising=False)
+    with pytest.raises(ValueError, match="No preprocessed files"):
+        ds.build_dataset_from_preprocessed(subject=1)
+    with pytest.raises(ValueError, match="Unknown source"):
+        ds.build_dataset_from_preprocessed("zenodo", subject=1)
+    monkeypatch.setenv("EEGNET_SYNTHETIC", "1")
+    assert ds.build_dataset_from_preprocessed(subject=1).X.shape == (288, 22, 257)
+    # real files win over the synthetic generator; positional src as in the reference
+    X = np.random.default_rng(0).standard_normal((5, 22, 257))
+    np.savez(tmp_path / "A02E.npz", X=X, y=np.arange(5) % 4)
+    d = ds.build_dataset_from_preprocessed("kaggle", 2, "Eval")
+    assert np.array_equal(d.X, X) and d.y.tolist() == [0, 1, 2, 3, 0]
+    allv = ds.build_dataset_from_preprocessed(subject="all", mode="Eval")
+    assert allv.X.shape[0] == 8 * 288 + 5
 
 
 def test_synthetic_sessions_shape_and_determinism():
     from eegnetreplication_amd.dataset import build_dataset_from_preprocessed
-    a = build_dataset_from_preprocessed(3)
-    b = build_dataset_from_preprocessed(3)
-    e = build_dataset_from_preprocessed(3, mode="Eval")
+    a = build_dataset_from_preprocessed(subject=3, synthetic=True)
+    b = build_dataset_from_preprocessed(subject=3, synthetic=True)
+    e = build_dataset_from_preprocessed(subject=3, mode="Eval", synthetic=True)
     assert a.X.shape == (288, 22, 257) and a.X.dtype == np.float64
     assert np.array_equal(a.X, b.X) and np.array_equal(a.y, b.y)
     assert not np.array_equal(a.X, e.X)
@@ -82,3 +106,31 @@ def test_fold_batch_dispatch_chunks_units(monkeypatch):
     out = T_._run_units(specs, 3, "cuda", 3)
     assert [r["seed"] for r in out] == list(range(100, 107))
     assert calls == [("batch", [100, 101, 102]), ("batch", [103, 104, 105]), ("batch", [106])]
+
+
+def test_device_loader_matches_dataloader_shuffle():
+    """DeviceLoader(shuffle=True, generator=g) yields the batches DataLoader(batch_size=64,
+    shuffle=True, generator=g) yields (train.py:87-89: RandomSampler draws torch.randperm(n, g) per
+    epoch; default collate, drop_last=False) -- same trials, same order, over several epochs.
+    FoldBatch.epoch draws its permutation the same way (torch.randperm(n, generator=g))."""
+    import torch
+    from torch.utils.data import DataLoader
+    from eegnetreplication_amd.dataset import BCICI2ADataset, DeviceLoader
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((150, 3, 8))
+    y = rng.integers(0, 4, 150)
+    ref = DataLoader(BCICI2ADataset(X, y), batch_size=64, shuffle=True,
+                     generator=torch.Generator().manual_seed(7))
+    mine = DeviceLoader(X, y, 64, shuffle=True, device="cpu", generator=torch.Generator().manual_seed(7))
+    assert len(mine) == len(ref) == 3
+    for _ in range(3):
+        got = list(mine)
+        exp = list(ref)
+        assert [len(b[1]) for b in got] == [64, 64, 22]
+        for (xa, ya), (xb, yb) in zip(got, exp):
+            assert torch.equal(ya, yb)
+            assert torch.equal(xa, xb.float())
+    # unshuffled loaders (validation / test, train.py:88-89) keep the dataset order
+    plain = DataLoader(BCICI2ADataset(X, y), batch_size=64, shuffle=False)
+    for (xa, ya), (xb, yb) in zip(DeviceLoader(X, y, 64, device="cpu"), plain):
+        assert torch.equal(ya, yb) and torch.equal(xa, xb.float())
