@@ -59,7 +59,9 @@ def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C
     """Seeded SMR-like session: classes 0..3 = left hand / right hand / feet /
     tongue.  Hand imagery desynchronises the mu (8-12 Hz) and beta (18-26 Hz) rhythm over the
     contralateral sensorimotor cortex (C4 for left, C3 for right), feet over Cz, tongue weakly
-    everywhere; each subject gets its own strength and spatial mixing, on top of 1/f noise.
+    everywhere; each subject gets its own strength and spatial mixing, on top of 1/f noise.  The
+    effect sizes put the reference model's per-subject test accuracy in the 30-80 % range of the
+    reference's own BCI IV-2a reports, so accuracy comparisons are not saturated.
     Trials are standardised per channel like the reference's exponential moving standardisation."""
     sess = 0 if mode == "Train" else 1
     rng = np.random.default_rng(1000 * subject + 17 * sess + 3)
@@ -67,10 +69,10 @@ def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C
     y = np.repeat(np.arange(4), n // 4)
     y = rng.permutation(np.concatenate([y, rng.integers(0, 4, n - y.size)]))
     t = np.arange(T) / SFREQ
-    X = _pink_noise(rng, (n, C, T), T) * 1.5
+    X = _pink_noise(rng, (n, C, T), T) * 2.0
     mu_f = srng.uniform(9.0, 11.5)
     beta_f = srng.uniform(19.0, 24.0)
-    strength = srng.uniform(0.6, 1.4)
+    strength = srng.uniform(0.25, 0.6)      # tuned so the stock reference reaches ~30-80 %
     mix = np.eye(C) + 0.15 * srng.standard_normal((C, C))
     for i in range(n):
         ph = rng.uniform(0, 2 * np.pi, 2)
