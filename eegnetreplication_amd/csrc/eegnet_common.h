@@ -63,6 +63,10 @@ struct Geo {
     int ldsA, ldsB, ldsC, ldsD, ldsE, ldsI;
     // optional timeline instrumentation (eegnet_trace_enable): [pass][workgroup][TR_SLOTS] stamps
     unsigned long long* trace;
+    // F2 > 16 (eegnet_wide.hip): o-chunks of 16 rows, Gram electrode slice per chunk, block-2 rows
+    // padded to F2P (32 / 64), block-2 row stride; LDS (floats) of the wide kernels
+    int wide, NOC, CPC, F2P, RB;
+    int ldsWA, ldsWB, ldsWB2, ldsWC, ldsWD, ldsWE, ldsWI;
 };
 
 // timeline stamps: wall clock (100 MHz) at kernel phase boundaries, shader-clock phase sums (loop)

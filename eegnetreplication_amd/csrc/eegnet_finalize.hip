@@ -123,8 +123,9 @@ __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, doub
 __host__ __device__ constexpr int fin1_scratch_doubles(int K1, int F1, int F2, int C) {
     return K1 * K1 + K1 + 128 + (F1 * K1 + 2 * F1 + F2 * C + 2 * F1 + 2 * F2 + 1) / 2 + 2;
 }
-__host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1, int nparam) {
-    return K1 * K1 + K1 + 128 + F1 * K1 + (CF_COUNT * CSTR + nparam + 1) / 2 + 2;
+// (ng = the number of leading parameters fin5 itself differentiates: o_g2)
+__host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1, int ng) {
+    return K1 * K1 + K1 + 128 + F1 * K1 + (CF_COUNT * CSTR + ng + 1) / 2 + 2;
 }
 
 // after pass A: BN1 (model.py:32) and BN2 (model.py:47) batch statistics
@@ -427,6 +428,13 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
             adam_elem(&ap[j], gr, &am[j], &av[j], fa.b1, fa.b2, step_size, bc2s, fa.eps);
             fa.params[i] = ap[j]; fa.adam_m[i] = am[j]; fa.adam_v[i] = av[j];
         }
+    }
+    // parameters beyond the staged block (large models, e.g. EEGNet-16,4 at 64 x 512: 14,116)
+    for (int i = tid + nth * APT; i < g.nparam; i += nth) {
+        float pp = fa.params[i], mm = fa.adam_m[i], vv = fa.adam_v[i];
+        const float gr = i < g.o_g2 ? gL[i] : fa.grads[i];
+        adam_elem(&pp, gr, &mm, &vv, fa.b1, fa.b2, step_size, bc2s, fa.eps);
+        fa.params[i] = pp; fa.adam_m[i] = mm; fa.adam_v[i] = vv;
     }
     if (tid == 0) *fa.step = s;
 }

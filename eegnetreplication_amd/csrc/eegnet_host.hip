@@ -43,6 +43,8 @@ static int device_cus() {
 
 static unsigned long long* g_trace_buf = nullptr;     // eegnet_trace_enable
 
+static int make_geo_wide(Geo* g, bool launch);
+
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     if (!d) return fail(EEGNET_EINVAL, "dims is NULL");
     memset(g, 0, sizeof(*g));
@@ -112,11 +114,10 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->ldsB = std::max(g->ldsB, tail(g->nB, 0));
     g->ldsC = std::max(g->ldsC, tail(g->nC, 0));
     g->ldsD = std::max(g->ldsD, tail(g->nD, 0));
-    g->ldsE = std::max(g->ldsE, tail(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->nparam)));
+    g->ldsE = std::max(g->ldsE, tail(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->o_g2)));
+    g->wide = g->F2 > F2MAX ? 1 : 0;
+    if (g->wide) return make_geo_wide(g, launch);
     if (launch) {
-        if (g->F2 > F2MAX)
-            return fail(EEGNET_EINVAL, "F1*D = %d > %d: the row-per-wave train step covers F2 <= %d "
-                        "(EEGNet-16,4 needs the cfg5 kernels)", g->F2, F2MAX, F2MAX);
         if (g->C * g->T > NTH * MAXPF)
             return fail(EEGNET_EINVAL, "C*T = %d exceeds the %d-float prefetch of one trial", g->C * g->T,
                         NTH * MAXPF);
@@ -133,13 +134,55 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     return 0;
 }
 
+// F2 > 16: o-chunked streaming passes and whole-trial block-2 passes (eegnet_wide.hip)
+static int make_geo_wide(Geo* g, bool launch) {
+    const int cus = device_cus();
+    g->NOC = (g->F2 + 15) / 16;
+    g->CPC = (g->C + g->NOC - 1) / g->NOC;
+    g->F2P = g->F2 <= 32 ? 32 : 64;
+    g->RB = rb_stride(g->T1);
+    // streaming grid: one 1024-thread workgroup per CU, NOC per trial range; a multiple of 8 * NOC
+    // when it can be (the chunk workgroups of a range then share an XCD)
+    int G = std::min(g->B * g->NOC, cus);
+    G = std::max(g->NOC, G / g->NOC * g->NOC);
+    if (G >= 8 * g->NOC) G = G / (8 * g->NOC) * (8 * g->NOC);
+    g->gridS = G;
+    g->grid = std::min(g->B, cus);                      // block-2 passes and the eval forward
+    const int nf4 = rup(g->NF, 4);
+    auto tailw = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + fin); };
+    g->ldsWA = std::max((g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW,
+                        tailw(g->nA, std::max(NTH, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C))));
+    g->ldsWB = 16 * g->RS;
+    const int b2 = 2 * g->F2P * g->RB + g->F2P * K2;
+    g->ldsWB2 = std::max(b2 + NWB2 * 2 * 16, tailw(g->nB, 0));
+    g->ldsWC = std::max(b2 + nf4 + NWB2 * 4 + NWB2 * 2 * 16, tailw(g->nC, 0));
+    g->ldsWD = std::max(std::max(b2 + g->F2P * g->RB + nf4, 2 * MAXIW * NTB2), tailw(g->nD, 0));
+    g->ldsWE = std::max(std::max(2 * 16 * g->RS + rup(16 * g->T1, 4) + 8 * 16, NWW * 256 + 16 * (g->K1 + 2)),
+                        tailw(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->o_g2)));
+    g->ldsWI = 16 * g->RS + b2 + nf4 + 4 * g->F2P;
+    if (!launch) return 0;
+    if (g->C > 4 * KSW) return fail(EEGNET_EINVAL, "C = %d > %d", g->C, 4 * KSW);
+    if (g->CPC * g->T > NTW * MAXPF)
+        return fail(EEGNET_EINVAL, "ceil(C / ceil(F2/16)) * T = %d exceeds the %d-float Gram slice", g->CPC * g->T,
+                    NTW * MAXPF);
+    if (g->T1 > 16 * NTTW * (NWB2 / 4)) return fail(EEGNET_EINVAL, "T/4 = %d > %d", g->T1, 16 * NTTW * (NWB2 / 4));
+    if (g->NF > MAXNFW * NTB2) return fail(EEGNET_EINVAL, "F2*(T/32) = %d > %d", g->NF, MAXNFW * NTB2);
+    if (g->F2P * ((g->T1 + 3) / 4) > MAXIW * NTB2) return fail(EEGNET_EINVAL, "F2*T/16 too large");
+    if ((double)g->B * g->F2 * g->T1 >= 4294967296.0)
+        return fail(EEGNET_EINVAL, "B*F2*(T/4) must stay below 2^32 (dropout / mask indices)");
+    const int lmax = std::max(std::max(std::max(g->ldsWA, g->ldsWB), std::max(g->ldsWB2, g->ldsWC)),
+                              std::max(std::max(g->ldsWD, g->ldsWE), g->ldsWI));
+    if (lmax * 4 > LDS_MAX) return fail(EEGNET_EINVAL, "dims need %d B of LDS (> %d)", lmax * 4, LDS_MAX);
+    return 0;
+}
+
 static WsLayout make_layout(const Geo& g) {
     WsLayout L;
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = rupz(o + bytes, 256); return r; };
     L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
     L.partA = take((size_t)g.gridS * g.nA * 4);
-    L.partB = take((size_t)g.gridS * g.nB * 4);
+    L.partB = take((size_t)std::max(g.gridS, g.grid) * g.nB * 4);
     L.partC = take((size_t)g.grid * g.nC * 4);
     L.partD = take((size_t)g.grid * g.nD * 4);
     L.partE = take((size_t)g.gridS * g.nE * 4);
@@ -213,8 +256,19 @@ static void set_attrs_shape() {
     hipFuncSetAttribute((const void*)k_infer<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
+template <int K1>
+static void set_attrs_wide() {
+    for (const void* f : {(const void*)k_wpass_a<K1>, (const void*)k_wpass_b<K1>, (const void*)k_wpass_e<K1>,
+                          (const void*)k_winfer<K1>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+}
+
 static void ensure_attrs() {
     if (g_attr_done) return;
+    set_attrs_wide<32>();
+    set_attrs_wide<64>();
+    for (const void* f : {(const void*)k_wpass_b2, (const void*)k_wpass_c, (const void*)k_wpass_d})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
                           (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>,
                           (const void*)k_infer_bf16<8, true>})
@@ -252,9 +306,53 @@ static FinArgs fin_args(const WsLayout& L, char* ws, int tk, float* bn, float* g
 }
 
 
+// F2 > 16: passes A, B (no reduction), B2 (BN3 statistics)
+template <int K1>
+static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
+                            const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s) {
+    const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
+    const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
+    { PROF(KID_A); hipLaunchKernelGGL((k_wpass_a<K1>), dim3(g.gridS), dim3(NTW), g.ldsWA * 4, s, g, params, x,
+                                      (float*)(ws + L.partA), fa); } LAUNCH_CHECK("k_wpass_a");
+    { PROF(KID_B); hipLaunchKernelGGL((k_wpass_b<K1>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g, params,
+                                      (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2),
+                                      (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
+    { PROF(KID_B); hipLaunchKernelGGL(k_wpass_b2, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
+                                      (const float*)(ws + L.d2), (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
+    return 0;
+}
+
+template <int K1>
+static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* params, const float* x,
+                             const uint8_t* m2, const uint8_t* m3, const float* dlogits, const int64_t* labels,
+                             float* logits, float* grads, float* loss, int c_mode, const FinArgs* adam,
+                             hipStream_t s) {
+    const float* coef = (const float*)(ws + L.coef);
+    const float* dl = dlogits ? dlogits : (const float*)(ws + L.dl);
+    const FinArgs fc = fin_args(L, ws, TK_C, nullptr, grads, loss, 0, (c_mode & PC_CE) ? 1 : 0);
+    const FinArgs fd = fin_args(L, ws, TK_D, nullptr, grads, nullptr, 0, 0);
+    FinArgs fe = fin_args(L, ws, TK_E, nullptr, grads, nullptr, 0, 0);
+    if (adam) {
+        fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
+        fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
+    }
+    { PROF(KID_C); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
+                                      (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
+                                      (float*)(ws + L.partC), c_mode, fc); } LAUNCH_CHECK("k_wpass_c(bwd)");
+    { PROF(KID_D); hipLaunchKernelGGL(k_wpass_d, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
+                                      (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
+                                      m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd); }
+    LAUNCH_CHECK("k_wpass_d");
+    { PROF(KID_E); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
+                                      (const float*)params, coef, x, (const float*)(ws + L.dp2),
+                                      (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
+    return 0;
+}
+
 template <int K1>
 static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
                        const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s) {
+    if (g.wide) return run_forward_wide<K1>(g, L, ws, params, bn, x, m2, update_running, nbt, s);
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
 #define LAUNCH_A(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridS), dim3(NTB), g.ldsA * 4, s, \
@@ -275,6 +373,9 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                         const float* x, const uint8_t* m2, const uint8_t* m3, const float* dlogits,
                         const int64_t* labels, float* logits, float* grads, float* loss, int c_mode,
                         const FinArgs* adam, hipStream_t s) {
+    if (g.wide)
+        return run_backward_wide<K1>(g, L, ws, params, x, m2, m3, dlogits, labels, logits, grads, loss, c_mode,
+                                     adam, s);
     const float* coef = (const float*)(ws + L.coef);
     const float* dl = dlogits ? dlogits : (const float*)(ws + L.dl);
     const FinArgs fc = fin_args(L, ws, TK_C, nullptr, grads, loss, 0, (c_mode & PC_CE) ? 1 : 0);
@@ -412,6 +513,14 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     if (r) return r;
     FinArgs none;
     memset(&none, 0, sizeof(none));
+    if (g.wide) {
+        { PROF(KID_C); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params,
+                                          (const float*)(w + L.coef), (const float*)(w + L.d2), mask3,
+                                          (const float*)nullptr, (const int64_t*)nullptr, logits, (float*)nullptr,
+                                          (float*)nullptr, (int)PC_LOGITS, none); }
+        LAUNCH_CHECK("k_wpass_c(fwd)");
+        return 0;
+    }
 #define LAUNCH_CF(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwC), g.ldsC * 4, s, \
                        g, params, (const float*)(w + L.coef), (const float*)(w + L.d2), mask3, (const float*)nullptr, \
                        (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS, none)
@@ -452,6 +561,12 @@ int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const floa
     ensure_attrs();
     hipStream_t s = (hipStream_t)stream;
     PROF(KID_INFER);
+    if (g.wide) {
+        if (g.K1 == 32) hipLaunchKernelGGL(k_winfer<32>, dim3(g.grid), dim3(NTW), g.ldsWI * 4, s, g, params, bn_buffers, x, logits);
+        else hipLaunchKernelGGL(k_winfer<64>, dim3(g.grid), dim3(NTW), g.ldsWI * 4, s, g, params, bn_buffers, x, logits);
+        LAUNCH_CHECK("k_winfer");
+        return 0;
+    }
 #define LAUNCH_I(K, CC, TT, FF) hipLaunchKernelGGL((k_infer<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsI * 4, s, \
                                                    g, params, bn_buffers, x, logits)
     if (g.K1 == 32) EEG_DISPATCH(32, g, LAUNCH_I); else EEG_DISPATCH(64, g, LAUNCH_I);

@@ -1,0 +1,1226 @@
+// eegnet_wide.hip -- the EEGNet train step and fp32 eval forward for F2 = F1*D > 16 (BASELINE cfg5:
+// EEGNet-16,4 on 64ch x 512 high-density EEG; reference model.py:13,21-84 with F1=16, D=4).
+// Included by eegnet_kernels.hip (one translation unit).
+//
+// Same restructured algorithm as the F2 <= 16 passes (eegnet_stream.hip), re-laid out
+// for planes that no longer fit one workgroup's LDS next to the trial's x (64 x 512 fp32 = 128 KB):
+//
+//  * streaming passes (A, B, E: full-rate data) work on o-CHUNKS of 16 rows.  A workgroup owns one
+//    chunk j for a contiguous trial range, one row per wave (16 waves); the spatial GEMM's x operand
+//    is read from global memory (the NOC workgroups of one trial range share an XCD, so x comes
+//    from that XCD's L2 after the first of them), so LDS holds only the chunk's s / dy rows.
+//    Pass A also forms the lag-Gram of a 1/NOC slice of the electrodes, so every trial's Gram is
+//    built once in total.  Per-row partial sums stay in registers, as in the narrow passes.
+//  * block-2-rate passes (B2, C, D: [F2, T/4] planes) work on whole trials, 8 waves per workgroup;
+//    the F2 x F2 pointwise mix, its weight gradient and its input gradient run on
+//    v_mfma_f32_16x16x4_f32 (exact fp32 fmaf chains, as the spatial GEMM).
+//  * every reducing pass ends in the same ticketed fp64 grid reduction and finalize (fin1..fin5).
+//
+//   A   x -> Gram slice, s chunk -> v -> sum v, v^2                      fin1 (BN1, BN2 constants)
+//   B   x -> s chunk -> v -> BN2 -> ELU -> pool4 -> dropout -> d2, E1, E2   (no reduction)
+//   B2  d2 -> dw16 -> pw (MFMA) -> sum r, r^2                            fin2 (BN3 constants)
+//   C   d2 -> block2 -> BN3 -> ELU -> pool8 -> dropout -> FC [-> CE, dFC, BN3-bwd sums]   fin3
+//   D   d2 -> block2 bwd: dW3, dq (MFMA), dw2, dd2 -> dp2, BN2-bwd sums  fin4
+//   E   x -> s chunk, v, dy2 -> Q correlation, FIR^T -> dws GEMM (MFMA)  fin5 (+ Adam)
+//   eval: one fused kernel per trial (chunks of s / v, then block 2 and the head)
+
+namespace eeg {
+
+constexpr int NTW = 1024;              // threads of the wide streaming passes and the wide eval
+constexpr int NWW = NTW / 64;          // = 16 rows of an o-chunk, one per wave
+constexpr int NTB2 = 512;              // threads of the wide block-2 passes (8 waves)
+constexpr int NWB2 = NTB2 / 64;
+constexpr int LQW = 8;                 // left pad of block-2 rows (dw16 reads t-7, its transpose t+7)
+constexpr int KSW = 16;                // spatial GEMM k-steps: C <= 64
+constexpr int MAXNOC = 4;              // o-chunks: F2 <= 64
+constexpr int MAXKS3 = 16;             // pointwise k-steps: F2P <= 64
+constexpr int MAXNFW = 4;              // head features per thread of a block-2 pass: NF <= 4 * 512
+constexpr int MAXIW = 16;              // (row, quad) items per thread of pass D's dd2: F2P*T1/4 <= 16*512
+
+// block-2 row stride (floats): [LQW zeros | T1P | >= 8 zeros], = 16 mod 64 so the 4 rows of one
+// MFMA B-fragment read (lk = 0..3, 16 consecutive t each) fall on 4 disjoint 16-bank groups
+__host__ __device__ constexpr int rb_stride(int T1) {
+    const int t1p = (T1 + 15) & ~15;
+    int r = LQW + t1p + 8;
+    while (r % 64 != 16) r += 4;
+    return r;
+}
+
+// workgroup -> (o-chunk j, trial range [b0, b1)).  When the grid allows, the NOC chunk workgroups
+// of one trial range get blockIdx values equal mod 8 -- the same XCD -- so they share its L2 for x.
+__device__ __forceinline__ void wide_unit(const Geo& g, int& j, int& b0, int& b1) {
+    const int G = gridDim.x, bi = blockIdx.x, NOC = g.NOC;
+    const int nr = G / NOC;
+    int r;
+    if (G % (8 * NOC) == 0) {
+        const int xcd = bi & 7, slot = bi >> 3;
+        j = slot % NOC;
+        r = (slot / NOC) * 8 + xcd;
+    } else {
+        j = bi % NOC;
+        r = bi / NOC;
+    }
+    b0 = (int)((long long)r * g.B / nr);
+    b1 = (int)((long long)(r + 1) * g.B / nr);
+}
+
+// s[i][t] = sum_c ws[o0 + i][c] x[c][t] for the 16 rows of one chunk (v_mfma_f32_16x16x4_f32).
+// A = ws fragments in registers (lane l: ws[o0 + (l & 15)][4s + (l >> 4)], zero outside), B = x
+// from global memory (unconditional loads at clamped addresses, masked to zero).  Tiles
+// n = wave, wave + NWW, ...; rows land in S at [i * RS + LP + t] (t < 16 * NT16 <= RS - LP).
+__device__ __forceinline__ void spatial_chunk(const float* __restrict__ xb, const float (&aw)[KSW], float* Ss,
+                                              int C, int T, int NT16, int RS, int LP, int wave, int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+    const int ks = (C + 3) >> 2;
+    for (int n = wave; n < NT16; n += NWW) {
+        const int t = 16 * n + li;
+        const bool ton = t < T;
+        const int tc = ton ? t : T - 1;
+        float bv[KSW];
+#pragma unroll
+        for (int s = 0; s < KSW; ++s) {
+            const int c = 4 * s + lk;
+            const float v = xb[(size_t)(c < C ? c : C - 1) * T + tc];
+            bv[s] = (s < ks && c < C && ton) ? v : 0.f;
+        }
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KSW; ++s)
+            if (s < ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aw[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ss[(4 * lk + r) * RS + LP + t] = acc[r];
+    }
+}
+
+__device__ __forceinline__ void load_aw_chunk(const Geo& g, const float* __restrict__ prm, int o0, float (&aw)[KSW],
+                                              int lane) {
+    const int o = o0 + (lane & 15), lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < KSW; ++s) {
+        const int c = 4 * s + lk;
+        aw[s] = (o < g.F2 && c < g.C) ? prm[g.o_ws + o * g.C + c] : 0.f;
+    }
+}
+
+// ================================================================================================
+// Wide pass A: BN1 / BN2 batch statistics.  Same partial row as k_pass_a:
+//   [G0 K1][S0][H nH][Tl nTl][hs R][ts P][Sv F2][Sv2 F2]
+// LDS: Gram slice rows [CPC][RS] | s rows [16][RS] | wave partials [NWW][K1 + 3]
+// ================================================================================================
+template <int K1>
+__global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict__ prm,
+                                                 const float* __restrict__ x, float* __restrict__ part,
+                                                 FinArgs fa) {
+    using G_ = KG<K1>;
+    constexpr int LP = G_::LP;
+    constexpr int NEI = G_::template nei<NTW>();
+    const int C = g.C, T = g.T, F2 = g.F2, RS = g.RS, TQ = (T + 3) >> 2, NT16 = (T + 15) >> 4;
+    if (blockIdx.x == 0 && threadIdx.x < (TK_PASSES - 1) * NCNT)
+        __hip_atomic_store(fa.cnt + NCNT + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    int j, b0, b1;
+    wide_unit(g, j, b0, b1);
+    const int o0 = 16 * j;
+    const int c0 = j * g.CPC, nc = max(0, min(g.CPC, C - c0));      // this workgroup's Gram slice
+    float* Xg = sm;
+    float* Ss = Xg + g.CPC * RS;
+    float* red = Ss + 16 * RS;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < (g.CPC + 16) * RS; i += NTW) sm[i] = 0.f;
+    float aw[KSW];
+    load_aw_chunk(g, prm, o0, aw, lane);
+    const int o = o0 + wave;
+    const bool row_on = o < F2;
+    float tap[K1];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + ((row_on ? o : 0) / g.D) * K1 + k];
+    const int NO = (T + 7) >> 3;
+    float svl = 0.f, sv2l = 0.f, s0 = 0.f;
+    float G0[K1];
+#pragma unroll
+    for (int d = 0; d < K1; ++d) G0[d] = 0.f;
+    float eacc[NEI];
+    int ea[NEI], eb[NEI];
+#pragma unroll
+    for (int i = 0; i < NEI; ++i) {
+        eacc[i] = 0.f;
+        int e = tid + NTW * i;
+        ea[i] = -1; eb[i] = -1;
+        if (e < g.nH) {
+            int a = 0;
+            while (e >= g.R - a) { e -= g.R - a; ++a; }
+            ea[i] = a; eb[i] = a + e;
+        } else if ((e -= g.nH) < g.nTl) {
+            int u = 0;
+            while (e >= g.P - u) { e -= g.P - u; ++u; }
+            ea[i] = T - g.P + u; eb[i] = T - g.P + u + e;
+        } else if ((e -= g.nTl) < g.R) {
+            ea[i] = e;
+        } else if ((e -= g.R) < g.P) {
+            ea[i] = T - g.P + e;
+        } else {
+            ea[i] = -2;
+        }
+    }
+    constexpr int PFW = MAXPF;                     // slice floats per thread: CPC*T <= NTW*PFW
+    float pf[PFW];
+    if (b0 < b1 && nc > 0) x_prefetch<PFW, NTW>(x + ((size_t)b0 * C + c0) * T, nc, T, pf, tid);
+    __syncthreads();
+    if (nc > 0) x_store<PFW, NTW>(pf, nc, T, RS, LP, Xg, tid);
+    __syncthreads();
+    drain_prologue_loads();
+    for (int b = b0; b < b1; ++b) {
+        const int bn = b + 1;
+        if (bn < b1 && nc > 0) x_prefetch<PFW, NTW>(x + ((size_t)bn * C + c0) * T, nc, T, pf, tid);
+        spatial_chunk(x + (size_t)b * C * T, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+        for (int q = tid; q < nc * TQ; q += NTW) {
+            const int c = q / TQ, qq = q - c * TQ;
+            float w[4 * G_::NW];
+            lds_window<G_::NW>(Xg + c * RS + 4 * qq, w);
+            float a[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = (4 * qq + i < T) ? w[G_::OFF + i] : 0.f;
+            s0 += (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+            for (int d = 0; d < K1; ++d) {
+                float acc = G0[d];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = fmaf(a[i], w[G_::OFF + i + d], acc);
+                G0[d] = acc;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NEI; ++i) {
+            if (ea[i] >= 0) {
+                const float* xa = Xg + LP + ea[i];
+                float acc = 0.f;
+                if (eb[i] >= 0) {
+                    const float* xb2 = Xg + LP + eb[i];
+                    for (int c = 0; c < nc; ++c) acc = fmaf(xa[c * RS], xb2[c * RS], acc);
+                } else {
+                    for (int c = 0; c < nc; ++c) acc += xa[c * RS];
+                }
+                eacc[i] += acc;
+            }
+        }
+        __syncthreads();                                   // s rows complete, slice read for good
+        if (row_on) {
+            const float* row = Ss + wave * RS;
+            for (int oc = lane; oc < NO; oc += 64) {
+                float w[4 * G_::NW8];
+                lds_window<G_::NW8>(row + 8 * oc, w);
+                float v[8];
+                fir8<K1, G_::OFF>(w, tap, v);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
+            }
+        }
+        if (bn < b1 && nc > 0) x_store<PFW, NTW>(pf, nc, T, RS, LP, Xg, tid);
+        __syncthreads();                                   // next slice staged, s rows free
+    }
+
+    // ---- workgroup reduction -> one partial row (other chunks' Sv / Sv2 entries are zero) ----
+    float* row = part + (size_t)blockIdx.x * g.nA;
+    float* svw = red + NWW * (K1 + 1);               // [NWW][2]
+    {
+        constexpr int NR = (K1 + 3 + 3) / 4 * 4, NQ = NR / 4;   // [G0 K1][s0][sv][sv2][pad]
+        float rv[NR];
+#pragma unroll
+        for (int d = 0; d < K1; ++d) rv[d] = G0[d];
+        rv[K1] = s0; rv[K1 + 1] = svl; rv[K1 + 2] = sv2l;
+#pragma unroll
+        for (int i = K1 + 3; i < NR; ++i) rv[i] = 0.f;
+        wave_reduce<NR>(rv);
+        if ((lane & 15) == 0) {
+            const int r0 = (lane >> 4) * NQ;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int idx = q + r0;
+                if (idx <= K1) red[wave * (K1 + 1) + idx] = rv[q];
+                else if (idx <= K1 + 2) svw[2 * wave + idx - K1 - 1] = rv[q];
+            }
+        }
+    }
+    __syncthreads();
+    if (tid <= K1) {
+        float t = 0.f;
+        for (int w = 0; w < NWW; ++w) t += red[w * (K1 + 1) + tid];
+        pub(row + tid, t);
+    }
+#pragma unroll
+    for (int i = 0; i < NEI; ++i)
+        if (ea[i] != -2 && tid + NTW * i < g.nedge) pub(row + (K1 + 1 + tid + NTW * i), eacc[i]);
+    for (int q = tid; q < 2 * F2; q += NTW) {
+        const int oo = q < F2 ? q : q - F2, w = oo - o0;
+        const float v = (w >= 0 && w < NWW) ? svw[2 * w + (q < F2 ? 0 : 1)] : 0.f;
+        pub(row + (K1 + 1 + g.nedge + q), v);
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nA, fa, dsm)) fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa);
+}
+
+// ================================================================================================
+// Wide pass B: forward to the pooled block-2 input d2 = dropout(pool4(ELU(BN2(y2)))) and the pooled
+// ELU' sums E1 / E2 of the BN2 backward, per o-chunk.  No reduction (BN3's statistics are pass B2's).
+// ================================================================================================
+template <int K1>
+__global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict__ prm, const float* coef,
+                                                 const float* __restrict__ x, const uint8_t* __restrict__ mask2,
+                                                 float* __restrict__ d2g, float* __restrict__ E1g,
+                                                 float* __restrict__ E2g) {
+    using G_ = KG<K1>;
+    constexpr int LP = G_::LP;
+    const int C = g.C, T = g.T, F2 = g.F2, RS = g.RS, T1 = T >> 2, NT16 = (T + 15) >> 4;
+    const unsigned dk0 = drop_key(g, 0);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    int j, b0, b1;
+    wide_unit(g, j, b0, b1);
+    const int o0 = 16 * j;
+    float* Ss = sm;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < 16 * RS; i += NTW) sm[i] = 0.f;
+    float aw[KSW];
+    load_aw_chunk(g, prm, o0, aw, lane);
+    const int o = o0 + wave;
+    const bool row_on = o < F2;
+    const int oo = row_on ? o : 0;
+    float tap[K1];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + (oo / g.D) * K1 + k];
+    const float alh = coef[CF_AL2 * CSTR + oo], beh = coef[CF_BE2 * CSTR + oo];
+    const float gah = prm[g.o_g2 + oo], bth = prm[g.o_b2 + oo];
+    const int NO = (T + 7) >> 3;
+    __syncthreads();
+    drain_prologue_loads();
+    for (int b = b0; b < b1; ++b) {
+        spatial_chunk(x + (size_t)b * C * T, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+        __syncthreads();
+        if (row_on) {
+            const float* row = Ss + wave * RS;
+            const size_t rb = ((size_t)b * F2 + o) * T1;
+            for (int oc = lane; oc < NO; oc += 64) {
+                float w[4 * G_::NW8];
+                lds_window<G_::NW8>(row + 8 * oc, w);
+                float v[8];
+                fir8<K1, G_::OFF>(w, tap, v);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int q = 2 * oc + h;
+                    float pe = 0.f, e1 = 0.f, e2 = 0.f;
+#pragma unroll
+                    for (int i = 4 * h; i < 4 * h + 4; ++i) {
+                        const float xh = fmaf(alh, v[i], beh);
+                        const float z = fmaf(gah, xh, bth);
+                        const float dz = elu_d(z);
+                        pe += z > 0.f ? z : dz - 1.f;
+                        e1 += dz;
+                        e2 = fmaf(dz, xh, e2);
+                    }
+                    if (q < T1) {
+                        d2g[rb + q] = pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q));
+                        E1g[rb + q] = e1;
+                        E2g[rb + q] = e2;
+                    }
+                }
+            }
+        }
+        __syncthreads();                                   // s rows free
+    }
+}
+
+// ================================================================================================
+// Block-2-rate helpers (whole trial per 512-thread workgroup, F2P = 16 * NJT rows, NJT in {2, 4})
+// ================================================================================================
+// pointwise tile ownership: wave w -> row tile jt = w % NJT, time tiles n = w / NJT + (8 / NJT) i
+struct B2Map {
+    int jt, n0, dn;
+};
+__device__ __forceinline__ B2Map b2_map(int NJT, int wave) {
+    B2Map m;
+    m.jt = wave % NJT;
+    m.n0 = wave / NJT;
+    m.dn = NWB2 / NJT;
+    return m;
+}
+
+// stage trial b's [F2][T1] rows of a global plane into padded LDS rows [F2P][RB] (pads untouched)
+__device__ __forceinline__ void b2_stage(const float* __restrict__ src, int F2, int T1, int RB, float* dst,
+                                         int tid) {
+    const int n = F2 * T1;
+    if ((T1 & 3) == 0) {
+        const int TQ1 = T1 >> 2;
+        for (int i = tid; i < n / 4; i += NTB2) {
+            const int o = i / TQ1, q = i - o * TQ1;
+            const float4 v = reinterpret_cast<const float4*>(src)[i];
+            lds_st4(dst + o * RB + LQW + 4 * q, (floatx4){v.x, v.y, v.z, v.w});
+        }
+    } else {
+        for (int i = tid; i < n; i += NTB2) {
+            const int o = i / T1, t = i - o * T1;
+            dst[o * RB + LQW + t] = src[i];
+        }
+    }
+}
+
+// q[o][t] = sum_k w2[o][k] d2[o][t + k - 7] (model.py:54-61, 'same', pad 7 | 8) for every row and
+// 4-sample quad: windows of 24 floats from the padded rows (start t - 8), taps from an LDS table
+__device__ __forceinline__ void b2_dw16(const float* D2, const float* W2s, float* Q, int F2, int T1, int RB,
+                                        int tid) {
+    const int TQ1 = (T1 + 3) >> 2;
+    for (int it = tid; it < F2 * TQ1; it += NTB2) {
+        const int o = it / TQ1, qd = it - o * TQ1;
+        float w[24];
+        lds_window<6>(D2 + o * RB + LQW + 4 * qd - 8, w);
+        float wt[K2];
+        lds_window<4>(W2s + o * K2, wt);
+        float out[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float a = 0.f;
+#pragma unroll
+            for (int k = 0; k < K2; ++k) a = fmaf(wt[k], w[1 + i + k], a);
+            out[i] = (4 * qd + i < T1) ? a : 0.f;
+        }
+        lds_st4(Q + o * RB + LQW + 4 * qd, (floatx4){out[0], out[1], out[2], out[3]});
+    }
+}
+
+// r[j][t] = sum_i W3[j][i] q[i][t] (model.py:62-69) for this wave's row tile and time tiles:
+// A = W3 fragments (registers a3[s]: W3[16 jt + (l & 15)][4 s + (l >> 4)]), B = q rows from LDS.
+// acc[i] is time tile n0 + dn * i.
+template <int NTT>
+__device__ __forceinline__ void b2_pw(const float* Q, const float (&a3)[MAXKS3], int KS3, int NT1, int RB,
+                                      const B2Map& mp, floatx4 (&acc)[NTT], int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < NTT; ++i) {
+        acc[i] = (floatx4){0.f, 0.f, 0.f, 0.f};
+        const int n = mp.n0 + mp.dn * i;
+        if (n < NT1) {
+            const float* qc = Q + lk * RB + LQW + 16 * n + li;
+#pragma unroll
+            for (int s = 0; s < MAXKS3; ++s)
+                if (s < KS3) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[s], qc[4 * s * RB], acc[i], 0, 0, 0);
+        }
+    }
+}
+
+__device__ __forceinline__ void load_a3(const Geo& g, const float* __restrict__ prm, int jt, float (&a3)[MAXKS3],
+                                        int lane) {
+    const int jj = 16 * jt + (lane & 15), lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < MAXKS3; ++s) {
+        const int i = 4 * s + lk;
+        a3[s] = (jj < g.F2 && i < g.F2) ? prm[g.o_W3 + jj * g.F2 + i] : 0.f;
+    }
+}
+
+// w2 taps [F2P][16] (zero rows beyond F2)
+__device__ __forceinline__ void load_w2s(const Geo& g, const float* __restrict__ prm, float* W2s, int F2P, int tid) {
+    for (int i = tid; i < F2P * K2; i += NTB2) W2s[i] = i < g.F2 * K2 ? prm[g.o_w2 + i] : 0.f;
+}
+
+// time tiles per wave of the block-2 MFMA loops: NT1 = ceil(T1 / 16) <= 16 (T <= 1024) over
+// 8 / NJT waves per row tile
+constexpr int NTTW = 8;
+
+// ================================================================================================
+// Wide pass B2: BN3 (model.py:71) batch statistics.  Partial row [Sr F2][Sr2 F2].
+// LDS: D2 [F2P][RB] | Q [F2P][RB] | W2s [F2P][16] | wave sums [NWB2][2][16]
+// ================================================================================================
+__global__ __launch_bounds__(NTB2) void k_wpass_b2(Geo g, const float* __restrict__ prm,
+                                                   const float* __restrict__ d2g, float* __restrict__ part,
+                                                   FinArgs fa) {
+    const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, RB = g.RB, NJT = F2P >> 4, KS3 = F2P >> 2;
+    const int NT1 = (T1 + 15) >> 4;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* D2 = sm;
+    float* Q = D2 + F2P * RB;
+    float* W2s = Q + F2P * RB;
+    float* ws_ = W2s + F2P * K2;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    for (int i = tid; i < 2 * F2P * RB; i += NTB2) sm[i] = 0.f;
+    load_w2s(g, prm, W2s, F2P, tid);
+    const B2Map mp = b2_map(NJT, wave);
+    float a3[MAXKS3];
+    load_a3(g, prm, mp.jt, a3, lane);
+    float sr[4] = {0.f, 0.f, 0.f, 0.f}, sr2[4] = {0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    drain_prologue_loads();
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid);
+        __syncthreads();
+        b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
+        __syncthreads();
+        floatx4 acc[NTTW];
+        b2_pw<NTTW>(Q, a3, KS3, NT1, RB, mp, acc, lane);
+#pragma unroll
+        for (int i = 0; i < NTTW; ++i) {
+            const int t = 16 * (mp.n0 + mp.dn * i) + li;
+            if (t < T1) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { sr[r] += acc[i][r]; sr2[r] = fmaf(acc[i][r], acc[i][r], sr2[r]); }
+            }
+        }
+        __syncthreads();                                   // D2 / Q free for the next trial
+    }
+    // rows 16 jt + 4 lk + r: sums over the 16 lanes li, then over the waves sharing jt
+    float v[8] = {sr[0], sr[1], sr[2], sr[3], sr2[0], sr2[1], sr2[2], sr2[3]};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = row_sum16(v[q]);
+    if (li == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            ws_[(wave * 2 + 0) * 16 + 4 * lk + r] = v[r];
+            ws_[(wave * 2 + 1) * 16 + 4 * lk + r] = v[4 + r];
+        }
+    }
+    __syncthreads();
+    float* row = part + (size_t)blockIdx.x * g.nB;
+    for (int q = tid; q < 2 * F2; q += NTB2) {
+        const int o = q < F2 ? q : q - F2, h = q < F2 ? 0 : 1, jt = o >> 4;
+        float a = 0.f;
+        for (int w = jt; w < NWB2; w += NJT) a += ws_[(w * 2 + h) * 16 + (o & 15)];
+        pub(row + q, a);
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nB, fa, dsm)) fin2(g, dsm + 2, fa);
+}
+
+// xh3 = BN3-normalised r (batch statistics of finalize 2) for this wave's rows, in place
+__device__ __forceinline__ void b2_bn3(const float* coef, const B2Map& mp, floatx4 (&acc)[NTTW], int lane,
+                                       float (&mu)[4], float (&inv)[4]) {
+    const int lk = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int jj = 16 * mp.jt + 4 * lk + r;
+        mu[r] = coef[CF_MU3 * CSTR + jj];
+        inv[r] = coef[CF_INV3 * CSTR + jj];
+    }
+#pragma unroll
+    for (int i = 0; i < NTTW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][r] = (acc[i][r] - mu[r]) * inv[r];
+}
+
+// ================================================================================================
+// Wide pass C: head (model.py:71-84).  logits, and (PC_BWD) CE, classifier grads, BN3-bwd sums.
+// Partial row [dWfc 4*NF][dbfc 4][Sdz3 F2][Sdz3x F2][loss].
+// LDS: D2 | Q | W2s | H [NF] (features, then their gradients) | class partials [NWB2][4] | sums
+// ================================================================================================
+__global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict__ prm, const float* coef,
+                                                  const float* __restrict__ d2g, const uint8_t* __restrict__ mask3,
+                                                  const float* __restrict__ dlin, const int64_t* __restrict__ labels,
+                                                  float* __restrict__ logits, float* __restrict__ dlout,
+                                                  float* __restrict__ part, int mode, FinArgs fa) {
+    const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, T2 = g.T2, NF = g.NF, RB = g.RB;
+    const int NJT = F2P >> 4, KS3 = F2P >> 2, NT1 = (T1 + 15) >> 4;
+    const unsigned dk1 = drop_key(g, 1);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* D2 = sm;
+    float* Q = D2 + F2P * RB;
+    float* W2s = Q + F2P * RB;
+    float* H = W2s + F2P * K2;
+    float* lgs = H + ((NF + 3) & ~3);
+    float* ws_ = lgs + NWB2 * 4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    for (int i = tid; i < 2 * F2P * RB; i += NTB2) sm[i] = 0.f;
+    load_w2s(g, prm, W2s, F2P, tid);
+    const B2Map mp = b2_map(NJT, wave);
+    float a3[MAXKS3];
+    load_a3(g, prm, mp.jt, a3, lane);
+    float g3[4], b3[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int jj = 16 * mp.jt + 4 * lk + r, jc = jj < F2 ? jj : 0;
+        g3[r] = prm[g.o_g3 + jc]; b3[r] = prm[g.o_b3 + jc];
+    }
+    float wf[NCLS][MAXNFW], wacc[NCLS][MAXNFW];
+#pragma unroll
+    for (int n = 0; n < NCLS; ++n)
+#pragma unroll
+        for (int u = 0; u < MAXNFW; ++u) {
+            const int f = tid + NTB2 * u;
+            wf[n][u] = f < NF ? prm[g.o_Wfc + n * NF + f] : 0.f;
+            wacc[n][u] = 0.f;
+        }
+    float bfc[NCLS];
+#pragma unroll
+    for (int n = 0; n < NCLS; ++n) bfc[n] = prm[g.o_bfc + n];
+    float sdz[4] = {0.f, 0.f, 0.f, 0.f}, sdzx[4] = {0.f, 0.f, 0.f, 0.f};
+    float bacc[NCLS] = {0.f, 0.f, 0.f, 0.f}, lossacc = 0.f;
+    const float invB = 1.0f / (float)g.B;
+    __syncthreads();
+    drain_prologue_loads();
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid);
+        __syncthreads();
+        b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
+        __syncthreads();
+        floatx4 acc[NTTW];
+        b2_pw<NTTW>(Q, a3, KS3, NT1, RB, mp, acc, lane);
+        float mu[4], inv[4];
+        b2_bn3(coef, mp, acc, lane, mu, inv);
+        // ELU -> AvgPool(1,8) -> H (flattened index j*T2 + t/8, model.py:75)
+#pragma unroll
+        for (int i = 0; i < NTTW; ++i) {
+            const int n = mp.n0 + mp.dn * i;
+            const int t = 16 * n + li;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jj = 16 * mp.jt + 4 * lk + r;
+                float e = (n < NT1 && t < 8 * T2) ? elu_f(fmaf(g3[r], acc[i][r], b3[r])) : 0.f;
+                e = sum8_hi(e);
+                if ((lane & 7) == 7 && n < NT1 && t < 8 * T2 && jj < F2) H[jj * T2 + (t >> 3)] = e * 0.125f;
+            }
+        }
+        __syncthreads();                                   // H complete
+        float hv[MAXNFW], kp[MAXNFW];
+        float lg[NCLS] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < MAXNFW; ++u) {
+            const int f = tid + NTB2 * u;
+            kp[u] = f < NF ? keep_mul(g, mask3, dk1, (unsigned)(b * NF + f)) : 0.f;
+            hv[u] = f < NF ? H[f] * kp[u] : 0.f;                       // dropout (model.py:74)
+#pragma unroll
+            for (int n = 0; n < NCLS; ++n) lg[n] = fmaf(wf[n][u], hv[u], lg[n]);
+        }
+        wave_reduce<NCLS>(lg);                                         // lane 16n: class n
+        if ((lane & 15) == 0) lgs[wave * 4 + (lane >> 4)] = lg[0];
+        __syncthreads();
+        float L[NCLS];
+#pragma unroll
+        for (int n = 0; n < NCLS; ++n) {
+            float a = 0.f;
+            for (int w = 0; w < NWB2; ++w) a += lgs[w * 4 + n];
+            L[n] = a + bfc[n];
+        }
+        if ((mode & PC_LOGITS) && tid < NCLS)
+            logits[(size_t)b * NCLS + tid] = tid == 0 ? L[0] : tid == 1 ? L[1] : tid == 2 ? L[2] : L[3];
+        if (mode & PC_BWD) {
+            float dl[NCLS];
+            if (mode & PC_CE) {                                        // nn.CrossEntropyLoss, mean
+                const float mx = fmaxf(fmaxf(L[0], L[1]), fmaxf(L[2], L[3]));
+                float se = 0.f;
+#pragma unroll
+                for (int n = 0; n < NCLS; ++n) se += expf(L[n] - mx);
+                const float lse = mx + logf(se);
+                const int y = (int)labels[b];
+                const float Ly = y == 0 ? L[0] : y == 1 ? L[1] : y == 2 ? L[2] : L[3];
+                if (tid == 0) lossacc += lse - Ly;
+#pragma unroll
+                for (int n = 0; n < NCLS; ++n) dl[n] = (expf(L[n] - lse) - (n == y ? 1.f : 0.f)) * invB;
+                if (tid < NCLS)
+                    dlout[(size_t)b * NCLS + tid] = tid == 0 ? dl[0] : tid == 1 ? dl[1] : tid == 2 ? dl[2] : dl[3];
+            } else {
+#pragma unroll
+                for (int n = 0; n < NCLS; ++n) dl[n] = dlin[(size_t)b * NCLS + n];
+            }
+            if (tid == 0)
+#pragma unroll
+                for (int n = 0; n < NCLS; ++n) bacc[n] += dl[n];
+#pragma unroll
+            for (int u = 0; u < MAXNFW; ++u) {
+                const int f = tid + NTB2 * u;
+                float d = 0.f;
+#pragma unroll
+                for (int n = 0; n < NCLS; ++n) {
+                    wacc[n][u] = fmaf(dl[n], hv[u], wacc[n][u]);
+                    d = fmaf(dl[n], wf[n][u], d);
+                }
+                if (f < NF) H[f] = d * kp[u];                           // dp3 (own slots)
+            }
+            __syncthreads();
+            // BN3-backward sums: dz3 = dp3 / 8 * ELU'(z3)
+#pragma unroll
+            for (int i = 0; i < NTTW; ++i) {
+                const int n = mp.n0 + mp.dn * i;
+                const int t = 16 * n + li;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int jj = 16 * mp.jt + 4 * lk + r;
+                    if (n < NT1 && t < 8 * T2 && jj < F2) {
+                        const float dz = H[jj * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3[r], acc[i][r], b3[r]));
+                        sdz[r] += dz;
+                        sdzx[r] = fmaf(dz, acc[i][r], sdzx[r]);
+                    }
+                }
+            }
+        }
+        __syncthreads();                                   // H, D2, Q free for the next trial
+    }
+    if (!(mode & PC_BWD)) return;
+    float* row = part + (size_t)blockIdx.x * g.nC;
+#pragma unroll
+    for (int n = 0; n < NCLS; ++n)
+#pragma unroll
+        for (int u = 0; u < MAXNFW; ++u) {
+            const int f = tid + NTB2 * u;
+            if (f < NF) pub(row + n * NF + f, wacc[n][u]);
+        }
+    float v[8] = {sdz[0], sdz[1], sdz[2], sdz[3], sdzx[0], sdzx[1], sdzx[2], sdzx[3]};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = row_sum16(v[q]);
+    if (li == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            ws_[(wave * 2 + 0) * 16 + 4 * lk + r] = v[r];
+            ws_[(wave * 2 + 1) * 16 + 4 * lk + r] = v[4 + r];
+        }
+    }
+    __syncthreads();
+    for (int q = tid; q < 2 * F2; q += NTB2) {
+        const int o = q < F2 ? q : q - F2, h = q < F2 ? 0 : 1, jt = o >> 4;
+        float a = 0.f;
+        for (int w = jt; w < NWB2; w += NJT) a += ws_[(w * 2 + h) * 16 + (o & 15)];
+        pub(row + NCLS * NF + NCLS + q, a);
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int n = 0; n < NCLS; ++n) pub(row + NCLS * NF + n, bacc[n]);
+        pub(row + NCLS * NF + NCLS + 2 * F2, lossacc);
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nC, fa, dsm)) fin3(g, prm, dsm + 2, fa);
+}
+
+// ================================================================================================
+// Wide pass D: block_2 backward -- dW3 and dq on the matrix cores, dw2, dd2 -> dropout -> dp2, and
+// the BN2-backward sums from pass B's pooled ELU' sums.  Partial row [dW3 F2*F2][dw2 F2*16][Sdz2 F2]
+// [Sdz2x F2].
+// LDS: D2 [F2P][RB] | Q [F2P][RB] (q, then dq) | DR [F2P][RB] | W2s | Hd [NF] | item sums
+// ================================================================================================
+__global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict__ prm, const float* coef,
+                                                  const float* __restrict__ d2g, const float* __restrict__ E1g,
+                                                  const float* __restrict__ E2g, const uint8_t* __restrict__ mask2,
+                                                  const uint8_t* __restrict__ mask3, const float* __restrict__ dl,
+                                                  float* __restrict__ dp2g, float* __restrict__ part, FinArgs fa) {
+    const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, T2 = g.T2, NF = g.NF, RB = g.RB;
+    const int NJT = F2P >> 4, KS3 = F2P >> 2, NT1 = (T1 + 15) >> 4, TQ1 = (T1 + 3) >> 2;
+    const unsigned dk0 = drop_key(g, 0), dk1 = drop_key(g, 1);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* D2 = sm;
+    float* Q = D2 + F2P * RB;
+    float* DR = Q + F2P * RB;
+    float* W2s = DR + F2P * RB;
+    float* Hd = W2s + F2P * K2;
+    float* isum = sm;                                   // [2][MAXIW][NTB2] item partials (after the loop)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    for (int i = tid; i < 3 * F2P * RB; i += NTB2) sm[i] = 0.f;
+    load_w2s(g, prm, W2s, F2P, tid);
+    const B2Map mp = b2_map(NJT, wave);
+    float a3[MAXKS3], a3t[MAXKS3];
+    load_a3(g, prm, mp.jt, a3, lane);
+    {   // W3^T fragments of row tile it = mp.jt: lane l holds W3[4 s + (l >> 4)][16 it + (l & 15)]
+        const int ii = 16 * mp.jt + li;
+#pragma unroll
+        for (int s = 0; s < MAXKS3; ++s) {
+            const int jj = 4 * s + lk;
+            a3t[s] = (ii < F2 && jj < F2) ? prm[g.o_W3 + jj * F2 + ii] : 0.f;
+        }
+    }
+    float g3[4], b3[4], A3[4], B3[4], C3[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int jj = 16 * mp.jt + 4 * lk + r, jc = jj < F2 ? jj : 0;
+        g3[r] = prm[g.o_g3 + jc]; b3[r] = prm[g.o_b3 + jc];
+        A3[r] = coef[CF_A3 * CSTR + jc]; B3[r] = coef[CF_B3 * CSTR + jc]; C3[r] = coef[CF_C3 * CSTR + jc];
+    }
+    float wf[NCLS][MAXNFW];
+#pragma unroll
+    for (int n = 0; n < NCLS; ++n)
+#pragma unroll
+        for (int u = 0; u < MAXNFW; ++u) {
+            const int f = tid + NTB2 * u;
+            wf[n][u] = f < NF ? prm[g.o_Wfc + n * NF + f] : 0.f;
+        }
+    // dW3 tiles of this wave: (jt, it) = q / NJT, q % NJT for q = wave + NWB2 m
+    constexpr int MW3 = 2;                              // NJT^2 / NWB2 <= 2
+    floatx4 accW[MW3];
+#pragma unroll
+    for (int m = 0; m < MW3; ++m) accW[m] = (floatx4){0.f, 0.f, 0.f, 0.f};
+    // dw2 item of this thread: row o2, taps 4 kq .. 4 kq + 3
+    const int o2 = tid >> 2, kq = tid & 3;
+    float acc2[4] = {0.f, 0.f, 0.f, 0.f};
+    // dd2 items: (row, quad) it = tid + NTB2 m -- a fixed row per (thread, m) across trials
+    float sz1[MAXIW], sz2[MAXIW];
+#pragma unroll
+    for (int m = 0; m < MAXIW; ++m) { sz1[m] = 0.f; sz2[m] = 0.f; }
+    __syncthreads();
+    drain_prologue_loads();
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+        float dlv[NCLS];
+#pragma unroll
+        for (int n = 0; n < NCLS; ++n) dlv[n] = dl[(size_t)b * NCLS + n];
+        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid);
+        // dh -> dropout -> dp3 (flattened) into Hd
+#pragma unroll
+        for (int u = 0; u < MAXNFW; ++u) {
+            const int f = tid + NTB2 * u;
+            float d = 0.f;
+#pragma unroll
+            for (int n = 0; n < NCLS; ++n) d = fmaf(dlv[n], wf[n][u], d);
+            if (f < NF) Hd[f] = d * keep_mul(g, mask3, dk1, (unsigned)(b * NF + f));
+        }
+        __syncthreads();
+        b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
+        __syncthreads();
+        {   // BN3 backward (finalize 3's batch constants): dr = A3 dz3 + B3 + C3 xh3 -> DR rows
+            floatx4 acc[NTTW];
+            b2_pw<NTTW>(Q, a3, KS3, NT1, RB, mp, acc, lane);
+            float mu[4], inv[4];
+            b2_bn3(coef, mp, acc, lane, mu, inv);
+#pragma unroll
+            for (int i = 0; i < NTTW; ++i) {
+                const int n = mp.n0 + mp.dn * i;
+                if (n >= NT1) continue;
+                const int t = 16 * n + li;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int jj = 16 * mp.jt + 4 * lk + r;
+                    const float xh = acc[i][r];
+                    const float dz = (t < 8 * T2 && jj < F2)
+                                         ? Hd[jj * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3[r], xh, b3[r])) : 0.f;
+                    const float d = (t < T1 && jj < F2) ? fmaf(A3[r], dz, fmaf(C3[r], xh, B3[r])) : 0.f;
+                    DR[jj * RB + LQW + t] = d;
+                }
+            }
+        }
+        __syncthreads();                                   // DR complete
+        // dW3[j][i] += sum_t dr[j][t] q[i][t] (float4 k-permuted operands; model.py:62-69 weight grad)
+#pragma unroll
+        for (int m = 0; m < MW3; ++m) {
+            const int q = wave + NWB2 * m;
+            if (q < NJT * NJT) {
+                const int jt = q / NJT, it = q - jt * NJT;
+                const float* ar = DR + (16 * jt + li) * RB + LQW + 4 * lk;
+                const float* br = Q + (16 * it + li) * RB + LQW + 4 * lk;
+                for (int kg = 0; kg < NT1; ++kg) {
+                    const floatx4 a4 = lds_ld4(ar + 16 * kg), b4 = lds_ld4(br + 16 * kg);
+                    accW[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], accW[m], 0, 0, 0);
+                    accW[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], accW[m], 0, 0, 0);
+                    accW[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], accW[m], 0, 0, 0);
+                    accW[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], accW[m], 0, 0, 0);
+                }
+            }
+        }
+        // dq[i][t] = sum_j W3[j][i] dr[j][t]: A = W3^T fragments, B = DR rows
+        floatx4 dq[NTTW];
+#pragma unroll
+        for (int i = 0; i < NTTW; ++i) {
+            dq[i] = (floatx4){0.f, 0.f, 0.f, 0.f};
+            const int n = mp.n0 + mp.dn * i;
+            if (n < NT1) {
+                const float* dc = DR + lk * RB + LQW + 16 * n + li;
+#pragma unroll
+                for (int s = 0; s < MAXKS3; ++s)
+                    if (s < KS3) dq[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a3t[s], dc[4 * s * RB], dq[i], 0, 0, 0);
+            }
+        }
+        __syncthreads();                                   // every reader of q is past: dq -> Q
+#pragma unroll
+        for (int i = 0; i < NTTW; ++i) {
+            const int n = mp.n0 + mp.dn * i;
+            if (n >= NT1) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Q[(16 * mp.jt + 4 * lk + r) * RB + LQW + 16 * n + li] = dq[i][r];
+        }
+        __syncthreads();
+        // dw2[o][k] += sum_t dq[o][t] d2p[o][t + k - 7]
+        if (o2 < F2) {
+            const float* dqr = Q + o2 * RB + LQW;
+            const float* d2r = D2 + o2 * RB + LQW - 8 + 4 * kq;     // d2p[t + k - 7] = d2r[t + 1 + k - 4 kq]
+            for (int tq = 0; tq < TQ1; ++tq) {
+                const floatx4 a4 = lds_ld4(dqr + 4 * tq);
+                const floatx4 w0 = lds_ld4(d2r + 4 * tq), w1 = lds_ld4(d2r + 4 * tq + 4);
+                const float w[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc2[kk] = fmaf(a4[i], w[1 + i + kk], acc2[kk]);
+            }
+        }
+        // dd2[t] = sum_k w2[k] dq[t + 7 - k] -> dropout -> dp2; BN2-backward sums (E1 / E2 of pass B)
+        const size_t rb = (size_t)b * F2 * T1;
+#pragma unroll
+        for (int m = 0; m < MAXIW; ++m) {
+            const int it = tid + NTB2 * m;
+            if (it >= F2 * TQ1) break;
+            const int o = it / TQ1, qd = it - o * TQ1;
+            float w[24];
+            lds_window<6>(Q + o * RB + LQW + 4 * qd - 8, w);              // dq[t - 8 .. t + 15]
+            float wt[K2];
+            lds_window<4>(W2s + o * K2, wt);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int t = 4 * qd + i;
+                float a = 0.f;
+#pragma unroll
+                for (int k = 0; k < K2; ++k) a = fmaf(wt[k], w[15 + i - k], a);
+                if (t < T1) {
+                    const size_t gi = rb + (size_t)o * T1 + t;
+                    const float dp = a * keep_mul(g, mask2, dk0, (unsigned)gi);
+                    dp2g[gi] = dp;
+                    sz1[m] = fmaf(dp * 0.25f, E1g[gi], sz1[m]);
+                    sz2[m] = fmaf(dp * 0.25f, E2g[gi], sz2[m]);
+                }
+            }
+        }
+        __syncthreads();                                   // D2, Q, DR, Hd free for the next trial
+    }
+    // ---- workgroup reduction ----
+    float* row = part + (size_t)blockIdx.x * g.nD;
+#pragma unroll
+    for (int m = 0; m < MW3; ++m) {
+        const int q = wave + NWB2 * m;
+        if (q < NJT * NJT) {
+            const int jt = q / NJT, it = q - jt * NJT;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jj = 16 * jt + 4 * lk + r, ii = 16 * it + li;
+                if (jj < F2 && ii < F2) pub(row + jj * F2 + ii, accW[m][r]);
+            }
+        }
+    }
+    if (o2 < F2) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) pub(row + F2 * F2 + o2 * K2 + 4 * kq + kk, acc2[kk]);
+    }
+    // item partials -> per-row sums in a fixed order (items of row o are it = o TQ1 + qd)
+#pragma unroll
+    for (int m = 0; m < MAXIW; ++m) {
+        isum[(0 * MAXIW + m) * NTB2 + tid] = sz1[m];
+        isum[(1 * MAXIW + m) * NTB2 + tid] = sz2[m];
+    }
+    __syncthreads();
+    for (int q = tid; q < 2 * F2; q += NTB2) {
+        const int o = q < F2 ? q : q - F2, h = q < F2 ? 0 : 1;
+        float a = 0.f;
+        for (int qd = 0; qd < TQ1; ++qd) {
+            const int it = o * TQ1 + qd, m = it / NTB2, th = it - m * NTB2;
+            a += isum[(h * MAXIW + m) * NTB2 + th];
+        }
+        pub(row + F2 * F2 + 16 * F2 + q, a);
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nD, fa, dsm)) fin4(g, prm, dsm + 2, fa);
+}
+
+// ================================================================================================
+// Wide pass E: dy2 and the weight-gradient reductions that need full-rate data, per o-chunk.
+// Partial row [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2] (other chunks' entries zero).
+// LDS: s rows, then e [16][RS] | dy rows [16][RS] | dp2 rows [16][T1] | coefficient table [16][8];
+// after the loop: dws tiles [NWW][256] and row sums
+// ================================================================================================
+template <int K1>
+__global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const float* coef,
+                                                 const float* __restrict__ x, const float* __restrict__ dp2g,
+                                                 float* __restrict__ part, FinArgs fa) {
+    using G_ = KG<K1>;
+    constexpr int LP = G_::LP;
+    const int C = g.C, T = g.T, F2 = g.F2, RS = g.RS, T1 = T >> 2, NT16 = (T + 15) >> 4;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    int j, b0, b1;
+    wide_unit(g, j, b0, b1);
+    const int o0 = 16 * j, nrows = min(16, F2 - o0);
+    float* Ss = sm;
+    float* Dys = Ss + 16 * RS;
+    float* DP = Dys + 16 * RS;
+    float* CT = DP + ((16 * T1 + 3) & ~3);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    for (int i = tid; i < 2 * 16 * RS; i += NTW) sm[i] = 0.f;
+    float aw[KSW];
+    load_aw_chunk(g, prm, o0, aw, lane);
+    const int o = o0 + wave;
+    const bool row_on = wave < nrows;
+    const int oo = row_on ? o : 0;
+    float tap[K1];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + (oo / g.D) * K1 + k];
+    if (tid < 8 * 16) {
+        const int r = tid >> 3, f = tid & 7, orr = min(o0 + r, F2 - 1);
+        const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
+                         : f == 2 ? prm + g.o_g2 : f == 3 ? prm + g.o_b2 : f == 4 ? coef + CF_AO * CSTR
+                         : f == 5 ? coef + CF_BO * CSTR : coef + CF_CO * CSTR;
+        CT[tid] = src[orr];
+    }
+    const int NO = (T + 7) >> 3;
+    float sdyl = 0.f, sdyvl = 0.f;
+    float Qc[K1];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) Qc[k] = 0.f;
+    // dws GEMM split: wave -> (c-tile ct, k-group range)
+    const int NCT = (C + 15) >> 4, wpc = NWW / NCT;
+    const bool gemm_on = wave < wpc * NCT;
+    const int ct = gemm_on ? wave / wpc : 0, pt = gemm_on ? wave - ct * wpc : 0;
+    const int kg0 = (NT16 * pt) / wpc, kg1 = gemm_on ? (NT16 * (pt + 1)) / wpc : 0;
+    floatx4 xacc = {0.f, 0.f, 0.f, 0.f};
+    const int ndp = nrows * T1;
+    __syncthreads();
+    drain_prologue_loads();
+    for (int b = b0; b < b1; ++b) {
+        for (int i = tid; i < ndp; i += NTW) DP[i] = dp2g[((size_t)b * F2 + o0) * T1 + i];
+        spatial_chunk(x + (size_t)b * C * T, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+        __syncthreads();                                   // s rows, dp2 rows complete
+        if (row_on) {
+            const float* row = Ss + wave * RS;
+            float* drow = Dys + wave * RS + LP;
+            const floatx4 c0v = lds_ld4(CT + 8 * wave), c1v = lds_ld4(CT + 8 * wave + 4);
+            const float alh = c0v[0], beh = c0v[1], gah = c0v[2], bth = c0v[3];
+            const float Aoh = c1v[0], Boh = c1v[1], Coh = c1v[2];
+            for (int oc = lane; oc < NO; oc += 64) {
+                float w[4 * G_::NW8];
+                lds_window<G_::NW8>(row + 8 * oc, w);
+                float v[8];
+                fir8<K1, G_::OFF>(w, tap, v);
+                float dpq[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) dpq[h] = (2 * oc + h < T1) ? DP[wave * T1 + 2 * oc + h] * 0.25f : 0.f;
+                float dy[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float xh = fmaf(alh, v[i], beh);
+                    const float z = fmaf(gah, xh, bth);
+                    const float dz = dpq[i >> 2] * elu_d(z);
+                    float d = fmaf(Aoh, dz, fmaf(Coh, xh, Boh));
+                    d = (8 * oc + i < T) ? d : 0.f;
+                    dy[i] = d;
+                    sdyl += d;
+                    sdyvl = fmaf(d, v[i], sdyvl);
+                }
+#pragma unroll
+                for (int k = 0; k < K1; ++k)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) Qc[k] = fmaf(dy[i], w[G_::OFF + i + k], Qc[k]);
+                lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
+                lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
+            }
+        }
+        wave_lds_fence();                                  // dy row complete; s row consumed
+        if (row_on) {                                      // e = FIR^T(dy) -> this wave's s row
+            const float* dyr = Dys + wave * RS;
+            float* erow = Ss + wave * RS + LP;
+            for (int oc = lane; oc < NO; oc += 64) {
+                float w[4 * G_::NW8];
+                lds_window<G_::NW8>(dyr + 8 * oc, w);
+                float e[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) e[i] = 0.f;
+#pragma unroll
+                for (int m = 0; m < K1; ++m)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) e[i] = fmaf(tap[K1 - 1 - m], w[G_::OFFD + i + m], e[i]);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
+                lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
+                lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+            }
+        }
+        __syncthreads();                                   // e rows complete
+        // Xm[o][c] += sum_t e[o][t] x[c][t]: A = e rows (LDS), B = x (global), float4 k-permuted
+        if (gemm_on) {
+            const int c = ct * 16 + li;
+            const bool bon = c < C;
+            const float* arow = Ss + li * RS + LP + 4 * lk;
+            const float* xr = x + ((size_t)b * C + (bon ? c : 0)) * T + 4 * lk;
+            for (int kg = kg0; kg < kg1; ++kg) {
+                const int t0 = 16 * kg + 4 * lk;
+                floatx4 b4;
+                if ((T & 3) == 0 && t0 + 3 < T) {
+                    b4 = *reinterpret_cast<const floatx4*>(xr + 16 * kg);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) b4[e] = (t0 + e < T) ? xr[16 * kg + e] : 0.f;
+                }
+                if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                const floatx4 a4 = lds_ld4(arow + 16 * kg);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
+            }
+        }
+        __syncthreads();                                   // e rows and dp2 rows consumed
+    }
+
+    // ---- reductions ----
+    float* red = sm;                                       // [NWW][256] dws tiles | row sums
+    float* rsum = red + NWW * 256;                         // [16][K1 + 2]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[wave * 256 + (4 * lk + q) * 16 + li] = gemm_on ? xacc[q] : 0.f;
+    {
+        constexpr int NR = (K1 + 2 + 3) / 4 * 4, NQ = NR / 4;    // [Q K1][sdy][sdyv][pad]
+        float rv[NR];
+#pragma unroll
+        for (int k = 0; k < K1; ++k) rv[k] = Qc[k];
+        rv[K1] = sdyl; rv[K1 + 1] = sdyvl;
+#pragma unroll
+        for (int i = K1 + 2; i < NR; ++i) rv[i] = 0.f;
+        wave_reduce<NR>(rv);
+        if ((lane & 15) == 0) {
+            const int r0 = (lane >> 4) * NQ;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                if (q + r0 < K1 + 2) rsum[wave * (K1 + 2) + q + r0] = rv[q];
+        }
+    }
+    __syncthreads();
+    float* row = part + (size_t)blockIdx.x * g.nE;
+    const int nQ = F2 * K1, nX = F2 * C;
+    for (int p = tid; p < g.nE; p += NTW) {
+        float v = 0.f;
+        if (p < nQ) {                                       // Q[o][k]
+            const int oq = p / K1, k = p - oq * K1, w = oq - o0;
+            if (w >= 0 && w < nrows) v = rsum[w * (K1 + 2) + k];
+        } else if (p < nQ + nX) {                           // Xm[o][c]
+            const int pp = p - nQ, ox = pp / C, c = pp - ox * C, w = ox - o0;
+            if (w >= 0 && w < nrows) {
+                const int ct2 = c >> 4, cc = c & 15;
+                for (int ww = ct2 * wpc; ww < (ct2 + 1) * wpc; ++ww) v += red[ww * 256 + w * 16 + cc];
+            }
+        } else {                                            // Sdy, Sdyv
+            const int pp = p - nQ - nX, os = pp < F2 ? pp : pp - F2, w = os - o0;
+            if (w >= 0 && w < nrows) v = rsum[w * (K1 + 2) + K1 + (pp < F2 ? 0 : 1)];
+        }
+        pub(row + p, v);
+    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nE, fa, dsm)) fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa);
+}
+
+// ================================================================================================
+// Wide eval forward (model.py:91-99 with .eval(), F2 > 16): one trial per 1024-thread workgroup.
+// Per o-chunk: spatial GEMM -> FIR -> folded BN1/BN2 -> ELU -> pool4 into the d2 rows; then dw16,
+// pointwise (MFMA), BN3 (running statistics), ELU, pool8 and the classifier.
+// LDS: s rows [16][RS] | D2 [F2P][RB] | Q [F2P][RB] | W2s [F2P][16] | H [NF] | affine [F2P][4]
+// ================================================================================================
+template <int K1>
+__global__ __launch_bounds__(NTW) void k_winfer(Geo g, const float* __restrict__ prm, const float* __restrict__ bn,
+                                                const float* __restrict__ x, float* __restrict__ logits) {
+    using G_ = KG<K1>;
+    constexpr int LP = G_::LP;
+    const int C = g.C, T = g.T, F2 = g.F2, F2P = g.F2P, RS = g.RS, T1 = T >> 2, T2 = g.T2, NF = g.NF;
+    const int RB = g.RB, NT16 = (T + 15) >> 4, NT1 = (T1 + 15) >> 4, KS3 = F2P >> 2, NJT = F2P >> 4;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Ss = sm;
+    float* D2 = Ss + 16 * RS;
+    float* Q = D2 + F2P * RB;
+    float* W2s = Q + F2P * RB;
+    float* H = W2s + F2P * K2;
+    float* AF = H + ((NF + 3) & ~3);                   // [F2P][4]: al, be (BN1+BN2), s3, b3 (BN3)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    for (int i = tid; i < 16 * RS + 2 * F2P * RB; i += NTW) sm[i] = 0.f;
+    for (int i = tid; i < F2P * K2; i += NTW) W2s[i] = i < F2 * K2 ? prm[g.o_w2 + i] : 0.f;
+    const float* rm1 = bn;              const float* rv1 = bn + g.F1;
+    const float* rm2 = bn + 2 * g.F1;   const float* rv2 = rm2 + F2;
+    const float* rm3 = rm2 + 2 * F2;    const float* rv3 = rm3 + F2;
+    if (tid < F2P) {
+        const int oo = tid < F2 ? tid : 0, gg = oo / g.D;
+        const float a1 = prm[g.o_g1 + gg] / sqrtf(rv1[gg] + g.eps);
+        const float c1 = prm[g.o_b1 + gg] - a1 * rm1[gg];
+        float W = 0.f;
+        for (int c = 0; c < C; ++c) W += prm[g.o_ws + oo * C + c];
+        const float s2 = prm[g.o_g2 + oo] / sqrtf(rv2[oo] + g.eps);
+        const float s3 = prm[g.o_g3 + oo] / sqrtf(rv3[oo] + g.eps);
+        AF[4 * tid + 0] = a1 * s2;
+        AF[4 * tid + 1] = (c1 * W - rm2[oo]) * s2 + prm[g.o_b2 + oo];
+        AF[4 * tid + 2] = s3;
+        AF[4 * tid + 3] = prm[g.o_b3 + oo] - rm3[oo] * s3;
+    }
+    // pointwise tiles: wave w -> (row tile jt = w % NJT, time tiles n = w / NJT + (NWW / NJT) i)
+    const int jt = wave % NJT, n0 = wave / NJT, dn = NWW / NJT;
+    float a3[MAXKS3];
+    load_a3(g, prm, jt, a3, lane);
+    const int NO = (T + 7) >> 3;
+    __syncthreads();
+    for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
+        const float* xb = x + (size_t)b * C * T;
+        for (int j = 0; j < g.NOC; ++j) {
+            float aw[KSW];
+            load_aw_chunk(g, prm, 16 * j, aw, lane);
+            spatial_chunk(xb, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+            __syncthreads();
+            const int o = 16 * j + wave;
+            if (o < F2) {
+                float tap[K1];
+#pragma unroll
+                for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + (o / g.D) * K1 + k];
+                const float al = AF[4 * o], be = AF[4 * o + 1];
+                const float* row = Ss + wave * RS;
+                for (int oc = lane; oc < NO; oc += 64) {
+                    float w[4 * G_::NW8];
+                    lds_window<G_::NW8>(row + 8 * oc, w);
+                    float v[8];
+                    fir8<K1, G_::OFF>(w, tap, v);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int q = 2 * oc + h;
+                        float pe = 0.f;
+#pragma unroll
+                        for (int i = 4 * h; i < 4 * h + 4; ++i) pe += elu_f(fmaf(al, v[i], be));
+                        if (q < T1) D2[o * RB + LQW + q] = pe * 0.25f;
+                    }
+                }
+            }
+            __syncthreads();                               // s rows free, d2 rows of chunk j done
+        }
+        // depthwise 1x16 (model.py:54-61)
+        const int TQ1 = (T1 + 3) >> 2;
+        for (int it = tid; it < F2 * TQ1; it += NTW) {
+            const int o = it / TQ1, qd = it - o * TQ1;
+            float w[24];
+            lds_window<6>(D2 + o * RB + LQW + 4 * qd - 8, w);
+            float wt[K2];
+            lds_window<4>(W2s + o * K2, wt);
+            float out[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float a = 0.f;
+#pragma unroll
+                for (int k = 0; k < K2; ++k) a = fmaf(wt[k], w[1 + i + k], a);
+                out[i] = (4 * qd + i < T1) ? a : 0.f;
+            }
+            lds_st4(Q + o * RB + LQW + 4 * qd, (floatx4){out[0], out[1], out[2], out[3]});
+        }
+        __syncthreads();
+        // pointwise (MFMA), BN3 (eval), ELU, pool8 -> H
+        for (int n = n0; n < NT1; n += dn) {
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            const float* qc = Q + lk * RB + LQW + 16 * n + li;
+#pragma unroll
+            for (int s = 0; s < MAXKS3; ++s)
+                if (s < KS3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[s], qc[4 * s * RB], acc, 0, 0, 0);
+            const int t = 16 * n + li;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jj = 16 * jt + 4 * lk + r;
+                float e = (t < 8 * T2) ? elu_f(fmaf(AF[4 * jj + 2], acc[r], AF[4 * jj + 3])) : 0.f;
+                e = sum8_hi(e);
+                if ((lane & 7) == 7 && t < 8 * T2 && jj < F2) H[jj * T2 + (t >> 3)] = e * 0.125f;
+            }
+        }
+        __syncthreads();
+        if (wave < NCLS) {                                 // classifier (model.py:78-82)
+            float a = 0.f;
+            for (int i = lane; i < NF; i += 64) a = fmaf(prm[g.o_Wfc + wave * NF + i], H[i], a);
+            a = wave_sum(a);
+            if (lane == 0) logits[(size_t)b * NCLS + wave] = a + prm[g.o_bfc + wave];
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace eeg
