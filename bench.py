@@ -53,6 +53,135 @@ def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
     }
 
 
+def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
+    """The same for the F2 > 16 passes (csrc/eegnet_wide.hip, cfg5).  Bytes: x is read from HBM
+    once per streaming pass (the o-chunk workgroups of a trial share it through L2)."""
+    F2 = F1 * D
+    T1, T2 = T // 4, T // 128
+    npairs = K1 * (K1 - 1) // 2
+    sp = F2 * C * T
+    fir = F2 * T * K1
+    b2 = F2 * T1 * 16 + F2 * F2 * T1
+    xb = C * T * 4
+    row = F2 * T1 * 4
+    return {
+        "k_wpass_a": (2 * (sp + fir + C * T * K1 + 2 * C * npairs), xb),
+        "k_wpass_b": (2 * (sp + fir), xb + 3 * row),
+        "k_wpass_b2": (2 * b2, row),
+        "k_wpass_c": (2 * (b2 + 2 * 4 * F2 * T2), row + 16),
+        "k_wpass_d": (2 * (b2 + 2 * F2 * F2 * T1 + 2 * F2 * T1 * 16), 4 * row + 16),
+        "k_wpass_e": (2 * (sp + 3 * fir + sp), xb + row),
+    }
+
+
+def roofline_entry(name, fl, by, avg_s, traffic=None):
+    """Roofline of one kernel from its algorithmic FLOPs / bytes per launch and average duration:
+    FP32 (vector == f32 MFMA on gfx950) when its intensity is above the ridge, else HBM."""
+    ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    if fl / by >= ridge:
+        ach = fl / avg_s / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "kernel": name,
+                "avg_us": round(avg_s * 1e6, 2), "alg_flop_per_launch": fl, "alg_bytes_per_launch": by,
+                "note": "fp32 VALU + f32 MFMA share the 157.3 TFLOP/s FP32 peak on gfx950"}
+    ach = by / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": name,
+            "avg_us": round(avg_s * 1e6, 2), "alg_bytes_per_launch": by}
+
+
+def timed_steps(trainer, xs, ys, steps, alg, B, barrier, prof=True):
+    """Warm-up done by the caller.  An untimed 5-step survey brackets every kernel with HIP events
+    (per-kernel table, dominant kernel); the timed region brackets only the dominant one.  Steps
+    rotate over the distinct input buffers ``xs`` (so x comes from HBM, not the 256 MB MALL).
+    Returns (seconds, per-kernel survey table, dominant kernel, its (launches, ms) in the timed
+    region)."""
+    from eegnetreplication_amd import _lib
+    table, dom, kern = {}, None, {}
+    nx = len(xs)
+    if prof:
+        _lib.profile_enable(True)
+        for i in range(5):
+            trainer.step(xs[i % nx], ys[i % nx])
+        torch.cuda.synchronize()
+        table = _lib.profile_collect()
+        cand = {k: v for k, v in table.items() if k in alg}
+        dom = max(cand, key=lambda k: cand[k][1]) if cand else None
+        _lib.profile_enable(dom is not None, kernels=[dom] if dom else None)
+        trainer.step(xs[0], ys[0])          # fill the event pool outside the timed region
+        torch.cuda.synchronize()
+        _lib.profile_collect()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        trainer.step(xs[i % nx], ys[i % nx])
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if prof:
+        kern = _lib.profile_collect()
+        _lib.profile_enable(False)
+    return dt, table, dom, kern.get(dom) if dom else None
+
+
+def kernel_table(table, alg, B):
+    out = {}
+    tot_all = max(sum(v[1] for v in table.values()), 1e-12)
+    for name, (cnt, tot) in table.items():
+        avg_ms = tot / max(cnt, 1)
+        e = {"launches": cnt, "avg_us": round(1e3 * avg_ms, 2), "share": round(tot / tot_all, 4)}
+        if name in alg:
+            fl, by = alg[name]
+            e["alg_tflops"] = round(fl * B / (avg_ms * 1e-3) / 1e12, 2)
+            e["alg_gbs"] = round(by * B / (avg_ms * 1e-3) / 1e9, 1)
+        out[name] = e
+    return out
+
+
+def bench_train_cfg5(dev, B, steps, warmup, p=0.5):
+    """BASELINE cfg5 training leg: EEGNet-16,4 on synthetic 64ch x 512 trials, fp32, batch B, p=0.5
+    with on-device masks, one step = forward + CE + backward + clamps + Adam (eegnet_train_step over
+    the o-chunked wide passes).  3 distinct x buffers in rotation."""
+    from eegnetreplication_amd import EEGNet, FusedTrainer
+    C, T, F1, D = 64, 512, 16, 4
+    torch.manual_seed(5)
+    model = EEGNet(C, T, F1=F1, D=D, p=p).to(dev).train()
+    g = torch.Generator(device=dev).manual_seed(6)
+    xs = [torch.randn(B, C, T, device=dev, generator=g) for _ in range(3)]
+    ys = [torch.randint(0, 4, (B,), device=dev, generator=g) for _ in range(3)]
+    tr = FusedTrainer(model)
+    for i in range(warmup):
+        tr.step(xs[i % 3], ys[i % 3])
+    alg = kernel_algorithmic_wide(C, T, F1, D)
+    dt, table, dom, dk = timed_steps(tr, xs, ys, steps, alg, B, lambda: None)
+    roof = None
+    if dom and dk:
+        fl, by = alg[dom]
+        pmc = load_pmc()
+        roof = roofline_entry(dom, fl * B, by * B, dk[1] / dk[0] * 1e-3,
+                              pmc.get(dom, {}).get("hbm_bytes_per_launch") if B == 1024 else None)
+    fl_step = sum(v[0] for v in alg.values())
+    tps = B * steps / dt
+    return {"metric": "train trials/sec (fwd+CE+bwd+Adam) EEGNet-16,4 64ch x 512, fp32",
+            "value": round(tps, 1), "unit": "trials/s", "batch": B, "steps": steps,
+            "ms_per_step": round(1e3 * dt / steps, 4), "loss": round(float(tr.loss.item()), 5),
+            "implemented_flop_per_trial": fl_step,
+            "step_fp32_frac": round(fl_step * tps / (PEAK_FP32_TFLOPS * 1e12), 4),
+            "hbm_fraction": round(2 * C * T * 4 * tps / (PEAK_HBM_GBS * 1e9), 4),
+            "roofline": roof, "kernels": kernel_table(table, alg, B)}
+
+
+def load_pmc():
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            return json.load(f)
+    return {}
+
+
 def cpu_model_name():
     try:
         with open("/proc/cpuinfo") as f:
@@ -188,6 +317,9 @@ def main():
     ap.add_argument("--infer-batch", type=int, default=16384)
     ap.add_argument("--no-folds", action="store_true", help="skip the fold-batched real-protocol leg")
     ap.add_argument("--folds", type=int, default=16)
+    ap.add_argument("--nx", type=int, default=4, help="distinct x buffers rotated in the timed region")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 EEGNet-16,4 training leg")
+    ap.add_argument("--cfg5-batch", type=int, default=1024)
     args = ap.parse_args()
 
     from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
@@ -202,9 +334,13 @@ def main():
 
     torch.manual_seed(0)
     model = EEGNet(C, T, F1=8, D=2, p=0.5).to(dev).train()
-    rng = np.random.default_rng(1234 + rank)
-    x = torch.from_numpy(rng.standard_normal((B, C, T), dtype=np.float32)).to(dev)
-    y = torch.from_numpy(np.random.default_rng(1235 + rank).integers(0, 4, B)).to(dev)
+    # NX distinct synthetic batches in rotation (4 x 92 MB at cfg2 > the 256 MB MALL): a training
+    # loop reads a new batch every step, so x must come from HBM in the timed region too
+    xs, ys = [], []
+    for i in range(args.nx):
+        rng = np.random.default_rng(1234 + 100 * rank + i)
+        xs.append(torch.from_numpy(rng.standard_normal((B, C, T), dtype=np.float32)).to(dev))
+        ys.append(torch.from_numpy(np.random.default_rng(1235 + 100 * rank + i).integers(0, 4, B)).to(dev))
     trainer = DataParallelTrainer(model) if world > 1 else FusedTrainer(model)
 
     def barrier():
@@ -212,38 +348,10 @@ def main():
             dist.barrier()
 
     prof = not args.no_profile
-    for _ in range(args.warmup):
-        trainer.step(x, y)
+    for i in range(args.warmup):
+        trainer.step(xs[i % args.nx], ys[i % args.nx])
     alg = kernel_algorithmic(C, T)
-    table, dom = {}, None
-    if prof:
-        # untimed survey: every kernel bracketed by HIP events -> per-kernel table and the
-        # dominant kernel.  Inside the timed region only that kernel is bracketed (each bracket
-        # costs stream time: bracketing all of them cost ~14% of the step).
-        _lib.profile_enable(True)
-        for _ in range(5):
-            trainer.step(x, y)
-        torch.cuda.synchronize()
-        table = _lib.profile_collect()
-        cand = {k: v for k, v in table.items() if k in alg}
-        dom = max(cand, key=lambda k: cand[k][1]) if cand else None
-        _lib.profile_enable(dom is not None, kernels=[dom] if dom else None)
-        trainer.step(x, y)         # fill the event pool outside the timed region
-        torch.cuda.synchronize()
-        _lib.profile_collect()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.step(x, y)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    kern = _lib.profile_collect() if prof else {}
-    if prof:
-        _lib.profile_enable(False)
+    dt, table, dom, dk = timed_steps(trainer, xs, ys, args.steps, alg, B, barrier, prof)
     loss = float(trainer.loss.item())
 
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -254,42 +362,14 @@ def main():
     trials_per_s = world * B * args.steps / dt
 
     if rank == 0:
-        per_kernel = {}
-        for name, (cnt, tot) in table.items():
-            avg_ms = tot / max(cnt, 1)
-            e = {"launches": cnt, "avg_us": round(1e3 * avg_ms, 2),
-                 "share": round(tot / max(sum(v[1] for v in table.values()), 1e-12), 4)}
-            if name in alg:
-                fl, by = alg[name]
-                e["alg_tflops"] = round(fl * B / (avg_ms * 1e-3) / 1e12, 2)
-                e["alg_gbs"] = round(by * B / (avg_ms * 1e-3) / 1e9, 1)
-            per_kernel[name] = e
+        per_kernel = kernel_table(table, alg, B)
         roof = None
-        if dom is not None and dom in kern:
-            cnt, tot = kern[dom]
-            avg_s = tot / cnt * 1e-3
+        if dom is not None and dk:
             fl, by = alg[dom]
-            intensity = fl / by
-            ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
-            pmc = {}
-            pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc_path):
-                with open(pmc_path) as f:
-                    pmc = json.load(f)
-            traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc else None
-            if intensity >= ridge:
-                ach = fl * B / avg_s / 1e12
-                roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
-                        "traffic": traffic, "kernel": dom, "avg_us": round(avg_s * 1e6, 2),
-                        "alg_flop_per_launch": fl * B, "alg_bytes_per_launch": by * B,
-                        "note": "fp32 VALU + f32 MFMA share the 157.3 TFLOP/s FP32 peak on gfx950"}
-            else:
-                ach = by * B / avg_s / 1e9
-                roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
-                        "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic,
-                        "kernel": dom, "avg_us": round(avg_s * 1e6, 2),
-                        "alg_bytes_per_launch": by * B}
+            pmc = load_pmc()
+            roof = roofline_entry(dom, fl * B, by * B, dk[1] / dk[0] * 1e-3,
+                                  pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc else None)
+        impl_flop = sum(v[0] for v in alg.values())
         infer = None
         if not args.no_infer:
             infer = bench_infer_bf16(dev, args.infer_batch, 64, 512, 16, 4, steps=20, warmup=3)
@@ -298,12 +378,22 @@ def main():
             folds = bench_folds(dev, args.folds, 1440, epochs=2)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            threads = min(16, len(os.sched_getaffinity(0)))
+            # the box's CPU share for one GPU is 16 cores (OMP_NUM_THREADS=16 there); all of them,
+            # then one thread on a smaller batch of the same step
+            affinity = len(os.sched_getaffinity(0))
+            threads = min(16, affinity)
             v, secs = cpu_baseline(B, C, T, args.cpu_steps, threads)
+            v1, secs1 = cpu_baseline(512, C, T, 2, 1)
             cpu = {"value": round(v, 1), "unit": "trials/s", "cores": threads, "kind": "port",
                    "sample": f"{args.cpu_steps} train steps (fwd+CE+bwd+Adam) of B={B} x {C}x{T} "
-                             f"after 1 warm-up, {secs:.1f} s, torch {torch.__version__} CPU, "
-                             f"{cpu_model_name()}"}
+                             f"after 1 warm-up, {secs:.1f} s, {threads} threads (the box's CPU share; "
+                             f"{affinity} in the affinity mask), torch {torch.__version__} CPU, "
+                             f"{cpu_model_name()}",
+                   "one_thread": {"value": round(v1, 1), "unit": "trials/s", "cores": 1,
+                                  "sample": f"2 steps of B=512 x {C}x{T} after 1 warm-up, {secs1:.1f} s"}}
+        cfg5 = None
+        if not args.no_cfg5:
+            cfg5 = bench_train_cfg5(dev, args.cfg5_batch, steps=10, warmup=3)
         out = {
             "metric": "train trials/sec (fwd+bwd) EEGNet-8,2 22ch x 256",
             "value": round(trials_per_s, 1),
@@ -324,9 +414,13 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "hbm_fraction": round(ALG_BYTES_PER_TRIAL * trials_per_s / (PEAK_HBM_GBS * 1e9), 4),
+            "step_fp32_frac": round(impl_flop * trials_per_s / (PEAK_FP32_TFLOPS * 1e12), 4),
+            "implemented_flop_per_trial": impl_flop,
+            "x_buffers": args.nx,
             "ref_formulation_tflops": round(REF_FLOP_PER_TRIAL * trials_per_s / 1e12, 2),
             "kernels": per_kernel,
             "final_loss": round(loss, 5),
+            "cfg5_train": cfg5,
             "cfg5_infer_bf16": infer,
             "real_protocol_folds": folds,
         }

@@ -213,9 +213,12 @@ static void set_key(Geo* g, uint64_t seed, uint64_t offset) {
 }
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
-enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_INFER_BF16, KID_COUNT };
+enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_INFER_BF16,
+                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
-                                              "k_adam", "k_infer", "memset_tickets", "k_infer_bf16"};
+                                              "k_adam", "k_infer", "memset_tickets", "k_infer_bf16",
+                                              "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c", "k_wpass_d",
+                                              "k_wpass_e", "k_winfer"};
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { unsigned mask = 0; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
@@ -312,12 +315,12 @@ static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const flo
                             const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s) {
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
-    { PROF(KID_A); hipLaunchKernelGGL((k_wpass_a<K1>), dim3(g.gridS), dim3(NTW), g.ldsWA * 4, s, g, params, x,
+    { PROF(KID_WA); hipLaunchKernelGGL((k_wpass_a<K1>), dim3(g.gridS), dim3(NTW), g.ldsWA * 4, s, g, params, x,
                                       (float*)(ws + L.partA), fa); } LAUNCH_CHECK("k_wpass_a");
-    { PROF(KID_B); hipLaunchKernelGGL((k_wpass_b<K1>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g, params,
+    { PROF(KID_WB); hipLaunchKernelGGL((k_wpass_b<K1>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g, params,
                                       (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2),
                                       (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
-    { PROF(KID_B); hipLaunchKernelGGL(k_wpass_b2, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
+    { PROF(KID_WB2); hipLaunchKernelGGL(k_wpass_b2, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
                                       (const float*)(ws + L.d2), (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
     return 0;
 }
@@ -336,14 +339,14 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
         fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
     }
-    { PROF(KID_C); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
+    { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
                                       (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
                                       (float*)(ws + L.partC), c_mode, fc); } LAUNCH_CHECK("k_wpass_c(bwd)");
-    { PROF(KID_D); hipLaunchKernelGGL(k_wpass_d, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
+    { PROF(KID_WD); hipLaunchKernelGGL(k_wpass_d, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
                                       (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
                                       m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd); }
     LAUNCH_CHECK("k_wpass_d");
-    { PROF(KID_E); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
+    { PROF(KID_WE); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
                                       (const float*)params, coef, x, (const float*)(ws + L.dp2),
                                       (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
     return 0;
@@ -514,7 +517,7 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     FinArgs none;
     memset(&none, 0, sizeof(none));
     if (g.wide) {
-        { PROF(KID_C); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params,
+        { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params,
                                           (const float*)(w + L.coef), (const float*)(w + L.d2), mask3,
                                           (const float*)nullptr, (const int64_t*)nullptr, logits, (float*)nullptr,
                                           (float*)nullptr, (int)PC_LOGITS, none); }
@@ -560,13 +563,14 @@ int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const floa
     if (int r = check_ptrs(x, "x", logits, "logits")) return r;
     ensure_attrs();
     hipStream_t s = (hipStream_t)stream;
-    PROF(KID_INFER);
     if (g.wide) {
+        PROF(KID_WINFER);
         if (g.K1 == 32) hipLaunchKernelGGL(k_winfer<32>, dim3(g.grid), dim3(NTW), g.ldsWI * 4, s, g, params, bn_buffers, x, logits);
         else hipLaunchKernelGGL(k_winfer<64>, dim3(g.grid), dim3(NTW), g.ldsWI * 4, s, g, params, bn_buffers, x, logits);
         LAUNCH_CHECK("k_winfer");
         return 0;
     }
+    PROF(KID_INFER);
 #define LAUNCH_I(K, CC, TT, FF) hipLaunchKernelGGL((k_infer<K, CC, TT, FF>), dim3(g.grid), dim3(NTH), g.ldsI * 4, s, \
                                                    g, params, bn_buffers, x, logits)
     if (g.K1 == 32) EEG_DISPATCH(32, g, LAUNCH_I); else EEG_DISPATCH(64, g, LAUNCH_I);

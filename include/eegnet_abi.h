@@ -107,7 +107,7 @@ int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const floa
  * ui.py:35) on bf16 input x [B,C,T] (16-byte aligned when T % 8 == 0), bf16 MFMA operands and fp32
  * accumulation; params / bn_buffers / logits as for eegnet_forward_eval (fp32).  Covers every
  * supported (C, T, F1, D) whose trial fits one workgroup's LDS, including the F2 > 16 shapes the
- * fp32 train step refuses. */
+ * fp32 path runs through the wide kernels. */
 int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const float* bn_buffers,
                              const uint16_t* x, float* logits, void* stream);
 
@@ -130,7 +130,8 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
 
 /* Optional per-kernel device timing for benchmarks: `on` is a bitmask of kernel ids (bit i = the
  * i-th name eegnet_profile_collect reports: k_pass_a, k_pass_b, k_pass_c, k_pass_d, k_pass_e,
- * k_adam, k_infer, memset_tickets, k_infer_bf16; -1 = all, 0 = off).  Every selected kernel this
+ * k_adam, k_infer, memset_tickets, k_infer_bf16, k_wpass_a, k_wpass_b, k_wpass_b2, k_wpass_c,
+ * k_wpass_d, k_wpass_e, k_winfer; -1 = all, 0 = off; the k_w* kernels are the F2 > 16 path).  Every selected kernel this
  * thread launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect
  * synchronises them and reports, per kernel name (32-byte slots in `names`), launch count and
  * summed device ms; it returns the number of kernels in *n_out.  Not for use under hipGraph
