@@ -18,6 +18,13 @@ _lock = threading.Lock()
 _lib = None
 
 
+class Fold(ctypes.Structure):
+    """Mirror of ``eegnet_fold`` (include/eegnet_abi.h): one model of a fold-indexed step."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("params", "bn_buffers", "num_batches_tracked", "x", "labels",
+                                              "grads", "adam_state", "step", "losses", "ws")] + \
+               [("seed", ctypes.c_uint64)]
+
+
 class Dims(ctypes.Structure):
     """Mirror of ``eegnet_dims`` (include/eegnet_abi.h)."""
     _fields_ = [
@@ -45,6 +52,9 @@ _SIGS = {
                                          ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
                                          _vp, _vp, ctypes.c_int, _vp]),
+    "eegnet_train_step_folds": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.c_int, _vp, ctypes.c_int64,
+                                               ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
+                                               ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp]),
     "eegnet_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "eegnet_profile_collect": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp, ctypes.c_int, _vp]),
     "eegnet_trace_enable": (ctypes.c_int, [_vp]),

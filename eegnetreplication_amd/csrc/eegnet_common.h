@@ -169,6 +169,45 @@ struct FinArgs {
     float lr, b1, b2, eps;
 };
 
+// ticket blocks of the five passes in a workspace
+enum { TK_A = 0, TK_B, TK_C, TK_D, TK_E, TK_COUNT };
+
+// Fold-indexed launches (eegnet_train_step_folds): blockIdx.y is the fold; a fold's pointers come
+// from its eegnet_fold entry and its workspace regions sit at the same offsets in every workspace.
+struct WsOff {
+    unsigned long long cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl;
+};
+struct FoldCall {
+    const eegnet_fold* folds;     // nullptr: single-model launch (pointers from the kernel arguments)
+    long long row0, slot;         // first trial of the batch in every fold's epoch data; loss slot
+    unsigned long long koff;      // dropout key offset (key = mix(seed, koff + *step))
+    float lr, b1, b2, eps;        // Adam (pass E's finalize)
+    WsOff off;
+};
+
+__device__ __forceinline__ FinArgs fold_fin(const FoldCall& fc, const eegnet_fold& f, int tk, int update_running,
+                                            int ce, bool nbt, bool adam, int nparam) {
+    char* ws = (char*)f.ws;
+    FinArgs a;
+    a.part2 = (double*)(ws + fc.off.sums);
+    a.cnt = (unsigned*)(ws + fc.off.cnt) + tk * NCNT;
+    a.stats = (double*)(ws + fc.off.stats);
+    a.coef = (float*)(ws + fc.off.coef);
+    a.bn = f.bn_buffers;
+    a.grads = f.grads;
+    a.loss = f.losses ? f.losses + fc.slot : nullptr;
+    a.nbt = nbt ? f.num_batches_tracked : nullptr;
+    a.update_running = update_running;
+    a.ce = ce;
+    a.tpass = tk;
+    a.params = adam ? f.params : nullptr;
+    a.adam_m = adam ? f.adam_state : nullptr;
+    a.adam_v = adam ? f.adam_state + nparam : nullptr;
+    a.step = adam ? f.step : nullptr;
+    a.lr = fc.lr; a.b1 = fc.b1; a.b2 = fc.b2; a.eps = fc.eps;
+    return a;
+}
+
 // padded-row strides, shared by host (make_geo) and the compile-time-shape kernels
 __host__ __device__ constexpr int rup4(int a) { return (a + 3) & ~3; }
 __host__ __device__ constexpr int imax(int a, int b) { return a > b ? a : b; }
@@ -232,6 +271,10 @@ __device__ __forceinline__ unsigned long long mix_key_dev(unsigned long long see
 __device__ __forceinline__ unsigned drop_key(const Geo& g, int layer) {
     if (!g.keystep) return layer ? g.key1 : g.key0;
     const unsigned long long k = mix_key_dev(g.kseed, g.koff + (unsigned long long)(*g.keystep));
+    return layer ? (unsigned)(k >> 32) ^ 0x5BD1E995u : (unsigned)k;
+}
+__device__ __forceinline__ unsigned fold_drop_key(const FoldCall& fc, const eegnet_fold& f, int layer) {
+    const unsigned long long k = mix_key_dev(f.seed, fc.koff + (unsigned long long)(*f.step));
     return layer ? (unsigned)(k >> 32) ^ 0x5BD1E995u : (unsigned)k;
 }
 __device__ __forceinline__ float keep_mul(const Geo& g, const uint8_t* __restrict__ mask, unsigned key,

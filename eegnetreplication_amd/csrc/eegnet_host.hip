@@ -23,7 +23,6 @@ constexpr int LDS_MAX = 160 * 1024 - 256;
 static inline int rup(int a, int m) { return (a + m - 1) / m * m; }
 static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
 
-enum { TK_A = 0, TK_B, TK_C, TK_D, TK_E, TK_COUNT };
 constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 800 B, a multiple of 16
 
 struct WsLayout {
@@ -150,24 +149,22 @@ static int make_geo_wide(Geo* g, bool launch) {
     g->grid = std::min(g->B, cus);                      // block-2 passes and the eval forward
     const int nf4 = rup(g->NF, 4);
     auto tailw = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + fin); };
-    g->ldsWA = std::max((g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW,
+    const int awl = KSW * 64;                               // spatial GEMM fragment table
+    g->ldsWA = std::max((g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW + awl,
                         tailw(g->nA, std::max(NTH, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C))));
-    g->ldsWB = 16 * g->RS;
-    const int b2 = 2 * g->F2P * g->RB + g->F2P * K2;
+    g->ldsWB = 16 * g->RS + awl;
+    const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables
+    const int TQ1 = (g->T1 + 3) / 4;
     g->ldsWB2 = std::max(b2 + NWB2 * 2 * 16, tailw(g->nB, 0));
-    g->ldsWC = std::max(b2 + nf4 + NWB2 * 4 + NWB2 * 2 * 16, tailw(g->nC, 0));
-    g->ldsWD = std::max(std::max(b2 + g->F2P * g->RB + nf4, 2 * MAXIW * NTB2), tailw(g->nD, 0));
-    g->ldsWE = std::max(std::max(2 * 16 * g->RS + rup(16 * g->T1, 4) + 8 * 16, NWW * 256 + 16 * (g->K1 + 2)),
+    g->ldsWC = std::max(b2 + nf4 + NWB2 * 4 + NWB2 * 2 * 16 + g->F2P * g->RB, tailw(g->nC, 0));
+    g->ldsWD = std::max(b2 + g->F2P * g->RB + nf4 + 2 * g->F2 * TQ1, tailw(g->nD, 0));
+    g->ldsWE = std::max(std::max(2 * 16 * g->RS + rup(16 * g->T1, 4) + 8 * 16 + awl, NWW * 256 + 16 * (g->K1 + 2)),
                         tailw(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->o_g2)));
-    g->ldsWI = 16 * g->RS + b2 + nf4 + 4 * g->F2P;
+    g->ldsWI = 16 * g->RS + b2 + nf4 + 4 * g->F2P + g->NOC * awl;
     if (!launch) return 0;
     if (g->C > 4 * KSW) return fail(EEGNET_EINVAL, "C = %d > %d", g->C, 4 * KSW);
-    if (g->CPC * g->T > NTW * MAXPF)
-        return fail(EEGNET_EINVAL, "ceil(C / ceil(F2/16)) * T = %d exceeds the %d-float Gram slice", g->CPC * g->T,
-                    NTW * MAXPF);
     if (g->T1 > 16 * NTTW * (NWB2 / 4)) return fail(EEGNET_EINVAL, "T/4 = %d > %d", g->T1, 16 * NTTW * (NWB2 / 4));
     if (g->NF > MAXNFW * NTB2) return fail(EEGNET_EINVAL, "F2*(T/32) = %d > %d", g->NF, MAXNFW * NTB2);
-    if (g->F2P * ((g->T1 + 3) / 4) > MAXIW * NTB2) return fail(EEGNET_EINVAL, "F2*T/16 too large");
     if ((double)g->B * g->F2 * g->T1 >= 4294967296.0)
         return fail(EEGNET_EINVAL, "B*F2*(T/4) must stay below 2^32 (dropout / mask indices)");
     const int lmax = std::max(std::max(std::max(g->ldsWA, g->ldsWB), std::max(g->ldsWB2, g->ldsWC)),
@@ -251,11 +248,12 @@ static bool g_attr_done = false;
 template <int K1, int CC, int TT, int FF>
 static void set_attrs_shape() {
     const int lds = LDS_MAX;
-    hipFuncSetAttribute((const void*)k_pass_a<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipFuncSetAttribute((const void*)k_pass_b<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipFuncSetAttribute((const void*)k_pass_c<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipFuncSetAttribute((const void*)k_pass_d<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipFuncSetAttribute((const void*)k_pass_e<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    for (const void* f : {(const void*)k_pass_a<K1, CC, TT, FF>, (const void*)k_pass_b<K1, CC, TT, FF>,
+                          (const void*)k_pass_c<K1, CC, TT, FF>, (const void*)k_pass_d<K1, CC, TT, FF>,
+                          (const void*)k_pass_e<K1, CC, TT, FF>, (const void*)k_pass_a<K1, CC, TT, FF, true>,
+                          (const void*)k_pass_b<K1, CC, TT, FF, true>, (const void*)k_pass_c<K1, CC, TT, FF, true>,
+                          (const void*)k_pass_d<K1, CC, TT, FF, true>, (const void*)k_pass_e<K1, CC, TT, FF, true>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipFuncSetAttribute((const void*)k_infer<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
@@ -352,19 +350,26 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
     return 0;
 }
 
+// fc.folds != nullptr: fold-indexed launch over nf folds (grid y); the other pointers are unused
 template <int K1>
 static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
-                       const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s) {
+                       const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s,
+                       const FoldCall& fc = FoldCall{}, int nf = 1) {
     if (g.wide) return run_forward_wide<K1>(g, L, ws, params, bn, x, m2, update_running, nbt, s);
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
-#define LAUNCH_A(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridS), dim3(NTB), g.ldsA * 4, s, \
-                                                   g, params, x, (float*)(ws + L.partA), fa)
+#define LAUNCH_A(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsA * 4, s, \
+                                                   g, params, x, (float*)(ws + L.partA), fa, fc); \
+    else hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsA * 4, s, \
+                                                   g, params, x, (float*)(ws + L.partA), fa, fc)
     { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
     } LAUNCH_CHECK("k_pass_a");
-#define LAUNCH_B(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.gridS), dim3(NTB), g.ldsB * 4, s, \
+#define LAUNCH_B(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
                        g, params, (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), \
-                       (float*)(ws + L.E2), (float*)(ws + L.partB), fb)
+                       (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc); \
+    else hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
+                       g, params, (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), \
+                       (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc)
     { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
     } LAUNCH_CHECK("k_pass_b");
     return 0;
@@ -375,32 +380,41 @@ template <int K1>
 static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params,
                         const float* x, const uint8_t* m2, const uint8_t* m3, const float* dlogits,
                         const int64_t* labels, float* logits, float* grads, float* loss, int c_mode,
-                        const FinArgs* adam, hipStream_t s) {
+                        const FinArgs* adam, hipStream_t s, const FoldCall& fc = FoldCall{}, int nf = 1) {
     if (g.wide)
         return run_backward_wide<K1>(g, L, ws, params, x, m2, m3, dlogits, labels, logits, grads, loss, c_mode,
                                      adam, s);
     const float* coef = (const float*)(ws + L.coef);
     const float* dl = dlogits ? dlogits : (const float*)(ws + L.dl);
-    const FinArgs fc = fin_args(L, ws, TK_C, nullptr, grads, loss, 0, (c_mode & PC_CE) ? 1 : 0);
+    const FinArgs fcC = fin_args(L, ws, TK_C, nullptr, grads, loss, 0, (c_mode & PC_CE) ? 1 : 0);
     const FinArgs fd = fin_args(L, ws, TK_D, nullptr, grads, nullptr, 0, 0);
     FinArgs fe = fin_args(L, ws, TK_E, nullptr, grads, nullptr, 0, 0);
     if (adam) {
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
         fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
     }
-#define LAUNCH_CB(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwC), g.ldsC * 4, s, \
+#define LAUNCH_CB(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF, true>), dim3(g.grid, nf), dim3(64 * g.nwC), g.ldsC * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
-                       (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fc)
+                       (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc); \
+    else hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid, nf), dim3(64 * g.nwC), g.ldsC * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
+                       (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc)
     { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
     } LAUNCH_CHECK("k_pass_c(bwd)");
-#define LAUNCH_D(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwD), g.ldsD * 4, s, \
+#define LAUNCH_D(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, true>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
                        (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2), \
-                       (float*)(ws + L.partD), fd)
+                       (float*)(ws + L.partD), fd, fc); \
+    else hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
+                       (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2), \
+                       (float*)(ws + L.partD), fd, fc)
     { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
     } LAUNCH_CHECK("k_pass_d");
-#define LAUNCH_E(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridS), dim3(NTB), g.ldsE * 4, s, \
-                       g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe)
+#define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
+                       g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc); \
+    else hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
+                       g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc)
     { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
     } LAUNCH_CHECK("k_pass_e");
     return 0;
@@ -526,7 +540,8 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     }
 #define LAUNCH_CF(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwC), g.ldsC * 4, s, \
                        g, params, (const float*)(w + L.coef), (const float*)(w + L.d2), mask3, (const float*)nullptr, \
-                       (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS, none)
+                       (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS, none, \
+                       FoldCall{})
     { PROF(KID_C);
       if (g.K1 == 32) EEG_DISPATCH(32, g, LAUNCH_CF); else EEG_DISPATCH(64, g, LAUNCH_CF);
     } LAUNCH_CHECK("k_pass_c(fwd)");
@@ -657,6 +672,41 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     return g.K1 == 32
         ? run_backward<32>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, ap, s)
         : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, ap, s);
+}
+
+int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fold* folds, int64_t row0,
+                            int64_t slot, uint64_t offset, float lr, float beta1, float beta2, float eps,
+                            void* stream) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (g.wide) return fail(EEGNET_EINVAL, "eegnet_train_step_folds: F1*D = %d > 16 is not supported", g.F2);
+    if (nfolds < 1 || nfolds > 65535) return fail(EEGNET_EINVAL, "nfolds must be in [1, 65535] (got %d)", nfolds);
+    if (!folds) return fail(EEGNET_EINVAL, "folds is NULL");
+    if (row0 < 0 || slot < 0) return fail(EEGNET_EINVAL, "row0 / slot must be >= 0");
+    g.drop = g.p > 0.f ? 1 : 0;
+    set_key(&g, 0, offset);                           // the keep threshold (keys come per fold)
+    ensure_attrs();
+    const WsLayout L = make_layout(g);
+    FoldCall fc;
+    memset(&fc, 0, sizeof(fc));
+    fc.folds = folds;
+    fc.row0 = row0; fc.slot = slot; fc.koff = offset;
+    fc.lr = lr; fc.b1 = beta1; fc.b2 = beta2; fc.eps = eps;
+    fc.off = {L.cnt, L.partA, L.partB, L.partC, L.partD, L.partE, L.sums, L.stats, L.coef, L.d2, L.E1, L.E2,
+              L.dp2, L.dl};
+    hipStream_t s = (hipStream_t)stream;
+    FinArgs adam;                                     // non-null marker: pass E's finalize runs Adam
+    memset(&adam, 0, sizeof(adam));
+    char* w = nullptr;                                // every per-fold pointer comes from `folds`
+    int r = g.K1 == 32 ? run_forward<32>(g, L, w, nullptr, nullptr, nullptr, nullptr, 1, nullptr, s, fc, nfolds)
+                       : run_forward<64>(g, L, w, nullptr, nullptr, nullptr, nullptr, 1, nullptr, s, fc, nfolds);
+    if (r) return r;
+    const int mode = PC_BWD | PC_CE;
+    return g.K1 == 32
+        ? run_backward<32>(g, L, w, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           mode, &adam, s, fc, nfolds)
+        : run_backward<64>(g, L, w, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           mode, &adam, s, fc, nfolds);
 }
 
 int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream) {

@@ -195,7 +195,7 @@ __device__ __forceinline__ void pw_bn3(const Geo& g, const float* __restrict__ p
 // Per-wave LDS: Hs [NF] -- the flattened head features (model.py:75 Flatten order), then their
 // gradients.
 // ================================================================================================
-template <int K1, int CC, int TT, int FF>
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* __restrict__ prm,
                                                 const float* coef,    // the finalize writes it: no __restrict__
                                                 const float* __restrict__ d2g,
@@ -203,10 +203,25 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
                                                 const float* __restrict__ dlin,
                                                 const int64_t* __restrict__ labels,
                                                 float* __restrict__ logits, float* __restrict__ dlout,
-                                                float* __restrict__ part, int mode, FinArgs fa) {
+                                                float* __restrict__ part, int mode, FinArgs fa, FoldCall fc) {
     EEG_DIMS(g);
     TRACE(g, 2, TR_ENTRY);
-    const unsigned dk1 = drop_key(g, 1);
+    unsigned dk1;
+    if (FOLD) {
+        const eegnet_fold& f = fc.folds[blockIdx.y];
+        char* ws = (char*)f.ws;
+        prm = f.params;
+        coef = (const float*)(ws + fc.off.coef);
+        d2g = (const float*)(ws + fc.off.d2);
+        mask3 = nullptr; dlin = nullptr; logits = nullptr;
+        labels = f.labels + fc.row0;
+        dlout = (float*)(ws + fc.off.dl);
+        part = (float*)(ws + fc.off.partC);
+        fa = fold_fin(fc, f, TK_C, 0, 1, false, false, g.nparam);
+        dk1 = fold_drop_key(fc, f, 1);
+    } else {
+        dk1 = drop_key(g, 1);
+    }
     constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
     constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
     const int NFP = rup4(NF);
@@ -382,7 +397,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
 // part row: [dW3 F2*F2][dw2 F2*16][Sdz2 F2][Sdz2x F2]
 // Per-wave LDS rows (stride RSW): P0 d2 (pad LPD) | P1 q, then dq (pad LPQ) | P2 dr (pad LPQ) | Hs [NF].
 // ================================================================================================
-template <int K1, int CC, int TT, int FF>
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict__ prm,
                                                  const float* coef,    // the finalize writes it: no __restrict__
                                                  const float* __restrict__ d2g,
@@ -392,10 +407,28 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                                                  const uint8_t* __restrict__ mask3,
                                                  const float* __restrict__ dl,
                                                  float* __restrict__ dp2g, float* __restrict__ part,
-                                                 FinArgs fa) {
+                                                 FinArgs fa, FoldCall fc) {
     EEG_DIMS(g);
     TRACE(g, 3, TR_ENTRY);
-    const unsigned dk0 = drop_key(g, 0), dk1 = drop_key(g, 1);
+    unsigned dk0, dk1;
+    if (FOLD) {
+        const eegnet_fold& f = fc.folds[blockIdx.y];
+        char* ws = (char*)f.ws;
+        prm = f.params;
+        coef = (const float*)(ws + fc.off.coef);
+        d2g = (const float*)(ws + fc.off.d2);
+        E1g = (const float*)(ws + fc.off.E1); E2g = (const float*)(ws + fc.off.E2);
+        mask2 = nullptr; mask3 = nullptr;
+        dl = (const float*)(ws + fc.off.dl);
+        dp2g = (float*)(ws + fc.off.dp2);
+        part = (float*)(ws + fc.off.partD);
+        fa = fold_fin(fc, f, TK_D, 0, 0, false, false, g.nparam);
+        dk0 = fold_drop_key(fc, f, 0);
+        dk1 = fold_drop_key(fc, f, 1);
+    } else {
+        dk0 = drop_key(g, 0);
+        dk1 = drop_key(g, 1);
+    }
     constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
     constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
     const int RSW = TT ? row_stride_b2(TT / 4) : g.RSW;

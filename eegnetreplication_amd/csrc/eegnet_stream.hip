@@ -19,9 +19,14 @@ constexpr int WGPC = 2;                // workgroups per CU
 constexpr int WPEB = NWB * WGPC / 4;   // waves per SIMD: HIP's __launch_bounds__ second argument is
                                        // the minimum waves per execution unit (caps VGPRs at 128)
 
-// FIR work layout: half-wave h = lane >> 5 takes row 2w + h, its 32 lanes take 8 consecutive
-// samples each (octet oc = (lane & 31) + 32 m): both rows of a wave advance together, with two
-// independent 4-output chains per lane per window load.
+// FIR work layout: lane l takes row 2w + fir_row(l) and the 8 consecutive samples of octet
+// fir_oct(l) + 32 m: both rows of a wave advance together, with two independent 4-output chains per
+// lane per window load.  Each 16-lane group of a ds_read_b128 covers 8 octets of EACH row: octet
+// starts 8 floats apart repeat a bank group every 8 octets, and the other row's base is RS = 4 mod
+// 8 floats away, so the 16 windows of a group land on 16 disjoint bank quads (a half-wave per row
+// put octets oc and oc + 8 of one row in the same group: a 2-way conflict on every window read).
+__device__ __forceinline__ int fir_row(int lane) { return (lane >> 3) & 1; }
+__device__ __forceinline__ int fir_oct(int lane) { return (lane & 7) | ((lane >> 4) << 3); }
 #define EEG_NO(TT) ((TT) ? ((TT) + 7) / 8 : ((T + 7) >> 3))
 #define EEG_MO(TT) ((TT) ? (((TT) + 7) / 8 + 31) / 32 : 4)
 
@@ -96,13 +101,20 @@ __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict_
 //   hs / ts = head / tail sample sums       (window-sum corrections)
 //   Sv, Sv2 = sum v, sum v^2 per row o      (BN2: y2 = a1 v + c1 W)
 // ================================================================================================
-template <int K1, int CC, int TT, int FF>
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __restrict__ prm,
                                                       const float* __restrict__ x, float* __restrict__ part,
-                                                      FinArgs fa) {
+                                                      FinArgs fa, FoldCall fc) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 0, TR_ENTRY);
+    if (FOLD) {                                    // fold-indexed launch: this fold's pointers
+        const eegnet_fold& f = fc.folds[blockIdx.y];
+        prm = f.params;
+        x = f.x + fc.row0 * (long long)C * T;
+        part = (float*)((char*)f.ws + fc.off.partA);
+        fa = fold_fin(fc, f, TK_A, 1, 0, false, false, g.nparam);
+    }
     // every pass re-arms its own tickets when it finishes; pass A also clears those of the later
     // passes of this call (stream order), so a call never depends on how the previous one ended
     if (blockIdx.x == 0 && threadIdx.x < (TK_PASSES - 1) * NCNT)
@@ -220,12 +232,12 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         TRACE_PH(g, 0, 1, tph_);
         // v = 32-tap FIR of this wave's s rows; BN2 sums of v
         {
-            const int hr = lane >> 5, o = RPW * wave + hr;
+            const int hr = fir_row(lane), o = RPW * wave + hr;
             float tl[K1];
             half_taps<K1, NTS>(tap, hr, tl);
             if (o < F2) {
                 const float* row = Ss + o * RS;
-                for (int oc = lane & 31; oc < NO; oc += 32) {
+                for (int oc = fir_oct(lane); oc < NO; oc += 32) {
                     float w[4 * G_::NW8];
                     lds_window<G_::NW8>(row + 8 * oc, w);
                     float v[8];
@@ -255,8 +267,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         rv[K1] = s0;
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
-            rv[K1 + 1 + r] = (lane >> 5) == r ? svl : 0.f;
-            rv[K1 + 1 + RPW + r] = (lane >> 5) == r ? sv2l : 0.f;
+            rv[K1 + 1 + r] = fir_row(lane) == r ? svl : 0.f;
+            rv[K1 + 1 + RPW + r] = fir_row(lane) == r ? sv2l : 0.f;
         }
 #pragma unroll
         for (int i = K1 + 1 + 2 * RPW; i < NR; ++i) rv[i] = 0.f;
@@ -293,18 +305,32 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
 // part row: [Sr F2][Sr2 F2]
 // LDS: x rows | s rows | d2 rows (pad LP2) | q rows | weight table [w2 F2MAX x 16][W3 F2MAX x F2MAX]
 // ================================================================================================
-template <int K1, int CC, int TT, int FF>
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __restrict__ prm,
                                                       const float* coef,    // the finalize writes it: no __restrict__
                                                       const float* __restrict__ x,
                                                       const uint8_t* __restrict__ mask2,
                                                       float* __restrict__ d2g, float* __restrict__ E1g,
                                                       float* __restrict__ E2g, float* __restrict__ part,
-                                                      FinArgs fa) {
+                                                      FinArgs fa, FoldCall fc) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 1, TR_ENTRY);
-    const unsigned dk0 = drop_key(g, 0);
+    unsigned dk0;
+    if (FOLD) {
+        const eegnet_fold& f = fc.folds[blockIdx.y];
+        char* ws = (char*)f.ws;
+        prm = f.params;
+        coef = (const float*)(ws + fc.off.coef);
+        x = f.x + fc.row0 * (long long)C * T;
+        mask2 = nullptr;
+        d2g = (float*)(ws + fc.off.d2); E1g = (float*)(ws + fc.off.E1); E2g = (float*)(ws + fc.off.E2);
+        part = (float*)(ws + fc.off.partB);
+        fa = fold_fin(fc, f, TK_B, 1, 0, true, false, g.nparam);
+        dk0 = fold_drop_key(fc, f, 0);
+    } else {
+        dk0 = drop_key(g, 0);
+    }
     constexpr int NTS = FF ? 1 : RPW;
     const int D = FF ? 2 : g.D;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -336,10 +362,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     float sr[RPW], sr2[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) { sr[r] = 0.f; sr2[r] = 0.f; }
-    // BN2 constants of this lane's FIR row (half-wave hr = lane >> 5)
+    // BN2 constants of this lane's FIR row (fir_row)
     float alh, beh, gah, bth;
     {
-        const int o = RPW * wave + (lane >> 5), oo = o < F2 ? o : 0;
+        const int o = RPW * wave + fir_row(lane), oo = o < F2 ? o : 0;
         alh = coef[CF_AL2 * CSTR + oo]; beh = coef[CF_BE2 * CSTR + oo];
         gah = prm[g.o_g2 + oo]; bth = prm[g.o_b2 + oo];
     }
@@ -372,7 +398,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         // before that x_store would hold its vmcnt wait (loads and stores drain in order)
         constexpr int MO = EEG_MO(TT);
         float d2v[MO][2], e1v[MO][2], e2v[MO][2];
-        const int hr = lane >> 5, oh = RPW * wave + hr;
+        const int hr = fir_row(lane), oh = RPW * wave + hr;
         {
             float tl[K1];
             half_taps<K1, NTS>(tap, hr, tl);
@@ -381,7 +407,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
                 float* drow = D2s + oh * RS2 + LP2;
 #pragma unroll
                 for (int m = 0; m < MO; ++m) {
-                    const int oc = (lane & 31) + 32 * m;
+                    const int oc = fir_oct(lane) + 32 * m;
                     if (oc >= NO) break;
                     float w[4 * G_::NW8];
                     lds_window<G_::NW8>(row + 8 * oc, w);
@@ -429,7 +455,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         if (oh < F2) {
 #pragma unroll
             for (int m = 0; m < MO; ++m) {
-                const int oc = (lane & 31) + 32 * m;
+                const int oc = fir_oct(lane) + 32 * m;
                 if (oc >= NO) break;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -483,15 +509,25 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 // part row: [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2]
 // LDS: x rows | s rows, then e | dy rows | dp2 [F2][T1]; after the loop: dws tiles | lag tiles
 // ================================================================================================
-template <int K1, int CC, int TT, int FF>
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,   // Adam (finalize) writes it
                                                       const float* coef,    // the finalize writes it: no __restrict__
                                                       const float* __restrict__ x,
                                                       const float* __restrict__ dp2g,
-                                                      float* __restrict__ part, FinArgs fa) {
+                                                      float* __restrict__ part, FinArgs fa, FoldCall fc) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 4, TR_ENTRY);
+    if (FOLD) {
+        const eegnet_fold& f = fc.folds[blockIdx.y];
+        char* ws = (char*)f.ws;
+        prm = f.params;
+        coef = (const float*)(ws + fc.off.coef);
+        x = f.x + fc.row0 * (long long)C * T;
+        dp2g = (const float*)(ws + fc.off.dp2);
+        part = (float*)(ws + fc.off.partE);
+        fa = fold_fin(fc, f, TK_E, 0, 0, false, true, g.nparam);
+    }
     constexpr int NTS = FF ? 1 : RPW;
     const int D = FF ? 2 : g.D;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -593,7 +629,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             if (bn < b1) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 1, tph_);
         {
-            const int hr = lane >> 5, oh = RPW * wave + hr;
+            const int hr = fir_row(lane), oh = RPW * wave + hr;
             float tl[K1];
             half_taps<K1, NTS>(tap, hr, tl);
             if (oh < F2) {
@@ -602,7 +638,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 const floatx4 c0 = lds_ld4(CT + 8 * oh), c1 = lds_ld4(CT + 8 * oh + 4);
                 const float alh = c0[0], beh = c0[1], gah = c0[2], bth = c0[3];
                 const float Aoh = c1[0], Boh = c1[1], Coh = c1[2];
-                for (int oc = lane & 31; oc < NO; oc += 32) {
+                for (int oc = fir_oct(lane); oc < NO; oc += 32) {
                     float w[4 * G_::NW8];
                     lds_window<G_::NW8>(row + 8 * oc, w);
                     float v[8];
@@ -648,7 +684,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             if (oh < F2) {
                 const float* dyr = Dys + oh * RS;
                 float* erow = Ss + oh * RS + LP;
-                for (int oc = lane & 31; oc < NO; oc += 32) {
+                for (int oc = fir_oct(lane); oc < NO; oc += 32) {
                     float w[4 * G_::NW8];
                     lds_window<G_::NW8>(dyr + 8 * oc, w);
                     float e[8];
@@ -739,12 +775,19 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     // ---- reductions ----
     float* row = part + (size_t)blockIdx.x * g.nE;
     {
-        // per-row (half-wave) sums: [Q K1][sdy][sdyv][pad 2]
+        // per-row sums: [Q K1][sdy][sdyv][pad 2]; a row's lanes (fir_row) are first gathered into
+        // one half-wave (lane L of half h takes the lane that held octet L & 31 of row h)
         constexpr int NR = K1 + 4, NH = NR / 2;
         float rv[NR];
 #pragma unroll
         for (int k = 0; k < K1; ++k) rv[k] = Q[k];
         rv[K1] = sdyl; rv[K1 + 1] = sdyvl; rv[K1 + 2] = 0.f; rv[K1 + 3] = 0.f;
+        {
+            const int ocl = lane & 31;
+            const int src = (ocl & 7) | ((ocl >> 3) << 4) | ((lane >> 5) << 3);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) rv[k] = __shfl(rv[k], src, 64);
+        }
         half_reduce<NR>(rv);
         if ((lane & 15) == 0) {
             const int o = RPW * wave + (lane >> 5), off = ((lane >> 4) & 1) * NH;

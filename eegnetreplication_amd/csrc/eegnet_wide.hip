@@ -35,7 +35,6 @@ constexpr int KSW = 16;                // spatial GEMM k-steps: C <= 64
 constexpr int MAXNOC = 4;              // o-chunks: F2 <= 64
 constexpr int MAXKS3 = 16;             // pointwise k-steps: F2P <= 64
 constexpr int MAXNFW = 4;              // head features per thread of a block-2 pass: NF <= 4 * 512
-constexpr int MAXIW = 16;              // (row, quad) items per thread of pass D's dd2: F2P*T1/4 <= 16*512
 
 // block-2 row stride (floats): [LQW zeros | T1P | >= 8 zeros], = 16 mod 64 so the 4 rows of one
 // MFMA B-fragment read (lk = 0..3, 16 consecutive t each) fall on 4 disjoint 16-bank groups
@@ -65,10 +64,10 @@ __device__ __forceinline__ void wide_unit(const Geo& g, int& j, int& b0, int& b1
 }
 
 // s[i][t] = sum_c ws[o0 + i][c] x[c][t] for the 16 rows of one chunk (v_mfma_f32_16x16x4_f32).
-// A = ws fragments in registers (lane l: ws[o0 + (l & 15)][4s + (l >> 4)], zero outside), B = x
-// from global memory (unconditional loads at clamped addresses, masked to zero).  Tiles
-// n = wave, wave + NWW, ...; rows land in S at [i * RS + LP + t] (t < 16 * NT16 <= RS - LP).
-__device__ __forceinline__ void spatial_chunk(const float* __restrict__ xb, const float (&aw)[KSW], float* Ss,
+// A = ws fragments from an LDS table awl[KSW][64] (lane l of k-step s: ws[o0 + (l & 15)][4s + (l >> 4)],
+// zero outside), B = x from global memory (unconditional loads at clamped addresses, masked to
+// zero).  Tiles n = wave, wave + NWW, ...; rows land in S at [i * RS + LP + t] (t < 16 NT16 <= RS - LP).
+__device__ __forceinline__ void spatial_chunk(const float* __restrict__ xb, const float* awl, float* Ss,
                                               int C, int T, int NT16, int RS, int LP, int wave, int lane) {
     const int li = lane & 15, lk = lane >> 4;
     const int ks = (C + 3) >> 2;
@@ -86,19 +85,38 @@ __device__ __forceinline__ void spatial_chunk(const float* __restrict__ xb, cons
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KSW; ++s)
-            if (s < ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aw[s], bv[s], acc, 0, 0, 0);
+            if (s < ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(awl[64 * s + lane], bv[s], acc, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Ss[(4 * lk + r) * RS + LP + t] = acc[r];
     }
 }
 
-__device__ __forceinline__ void load_aw_chunk(const Geo& g, const float* __restrict__ prm, int o0, float (&aw)[KSW],
-                                              int lane) {
-    const int o = o0 + (lane & 15), lk = lane >> 4;
-#pragma unroll
-    for (int s = 0; s < KSW; ++s) {
-        const int c = 4 * s + lk;
-        aw[s] = (o < g.F2 && c < g.C) ? prm[g.o_ws + o * g.C + c] : 0.f;
+// the ws fragment table of chunk rows [o0, o0 + 16) into LDS (KSW * 64 floats)
+__device__ __forceinline__ void stage_aw_chunk(const Geo& g, const float* __restrict__ prm, int o0, float* awl,
+                                               int tid, int nth) {
+    for (int i = tid; i < KSW * 64; i += nth) {
+        const int s = i >> 6, l = i & 63, o = o0 + (l & 15), c = 4 * s + (l >> 4);
+        awl[i] = (o < g.F2 && c < g.C) ? prm[g.o_ws + o * g.C + c] : 0.f;
+    }
+}
+
+// x rows [c0, c0 + nc) of one trial into padded LDS rows (data window [LP, LP + T)): LDS-DMA of
+// 256-sample pieces when T is a multiple of 256 (no registers; drains at the next barrier), else a
+// plain copy
+__device__ __forceinline__ void stage_slice(const float* __restrict__ xs, int nc, int T, int RS, int LP, float* Xg,
+                                            int tid, int wave, int lane) {
+    if ((T & 255) == 0) {
+        const int np = T >> 8;
+        for (int i = wave; i < nc * np; i += NWW) {
+            const int c = i / np, p = i - c * np;
+            __builtin_amdgcn_global_load_lds((gvoid_t*)(xs + (size_t)c * T + 256 * p + 4 * lane),
+                                             (lvoid_t*)(Xg + c * RS + LP + 256 * p), 16, 0, 0);
+        }
+    } else {
+        for (int i = tid; i < nc * T; i += NTW) {
+            const int c = i / T, t = i - c * T;
+            Xg[c * RS + LP + t] = xs[i];
+        }
     }
 }
 
@@ -125,11 +143,11 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
     float* Xg = sm;
     float* Ss = Xg + g.CPC * RS;
     float* red = Ss + 16 * RS;
+    float* awl = red + NWW * (K1 + 1) + 2 * NWW;        // ws fragments [KSW][64]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < (g.CPC + 16) * RS; i += NTW) sm[i] = 0.f;
-    float aw[KSW];
-    load_aw_chunk(g, prm, o0, aw, lane);
+    stage_aw_chunk(g, prm, o0, awl, tid, NTW);
     const int o = o0 + wave;
     const bool row_on = o < F2;
     float tap[K1];
@@ -163,17 +181,13 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
             ea[i] = -2;
         }
     }
-    constexpr int PFW = MAXPF;                     // slice floats per thread: CPC*T <= NTW*PFW
-    float pf[PFW];
-    if (b0 < b1 && nc > 0) x_prefetch<PFW, NTW>(x + ((size_t)b0 * C + c0) * T, nc, T, pf, tid);
-    __syncthreads();
-    if (nc > 0) x_store<PFW, NTW>(pf, nc, T, RS, LP, Xg, tid);
+    __syncthreads();                                   // zero fill done before the first slice lands
+    if (b0 < b1 && nc > 0) stage_slice(x + ((size_t)b0 * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
     __syncthreads();
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
-        if (bn < b1 && nc > 0) x_prefetch<PFW, NTW>(x + ((size_t)bn * C + c0) * T, nc, T, pf, tid);
-        spatial_chunk(x + (size_t)b * C * T, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+        spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
         for (int q = tid; q < nc * TQ; q += NTW) {
             const int c = q / TQ, qq = q - c * TQ;
             float w[4 * G_::NW];
@@ -205,6 +219,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
             }
         }
         __syncthreads();                                   // s rows complete, slice read for good
+        if (bn < b1 && nc > 0) stage_slice(x + ((size_t)bn * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
         if (row_on) {
             const float* row = Ss + wave * RS;
             for (int oc = lane; oc < NO; oc += 64) {
@@ -217,7 +232,6 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
                     if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
             }
         }
-        if (bn < b1 && nc > 0) x_store<PFW, NTW>(pf, nc, T, RS, LP, Xg, tid);
         __syncthreads();                                   // next slice staged, s rows free
     }
 
@@ -279,11 +293,11 @@ __global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict_
     wide_unit(g, j, b0, b1);
     const int o0 = 16 * j;
     float* Ss = sm;
+    float* awl = Ss + 16 * RS;                         // ws fragments [KSW][64]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < 16 * RS; i += NTW) sm[i] = 0.f;
-    float aw[KSW];
-    load_aw_chunk(g, prm, o0, aw, lane);
+    stage_aw_chunk(g, prm, o0, awl, tid, NTW);
     const int o = o0 + wave;
     const bool row_on = o < F2;
     const int oo = row_on ? o : 0;
@@ -296,7 +310,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict_
     __syncthreads();
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
-        spatial_chunk(x + (size_t)b * C * T, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+        spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
         __syncthreads();
         if (row_on) {
             const float* row = Ss + wave * RS;
@@ -388,33 +402,39 @@ __device__ __forceinline__ void b2_dw16(const float* D2, const float* W2s, float
     }
 }
 
-// r[j][t] = sum_i W3[j][i] q[i][t] (model.py:62-69) for this wave's row tile and time tiles:
-// A = W3 fragments (registers a3[s]: W3[16 jt + (l & 15)][4 s + (l >> 4)]), B = q rows from LDS.
-// acc[i] is time tile n0 + dn * i.
+// r[j][t] = sum_i W3[j][i] q[i][t] (model.py:62-69) for one time tile n of row tile jt:
+// A = W3 fragments from the LDS table W3s [F2P][F2P + 1] (lane l of k-step s: W3[16 jt + (l & 15)]
+// [4 s + (l >> 4)]; the odd row stride keeps the 16 rows of a fragment on distinct banks), B = q
+// rows from LDS.
+__device__ __forceinline__ floatx4 b2_pw_tile(const float* Q, const float* W3s, int F2P, int jt, int n, int RB,
+                                              int lane) {
+    const int li = lane & 15, lk = lane >> 4, W3S = F2P + 1;
+    const float* qc = Q + lk * RB + LQW + 16 * n + li;
+    const float* ar = W3s + (16 * jt + li) * W3S + lk;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < MAXKS3; ++s)
+        if (4 * s < F2P) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[4 * s], qc[4 * s * RB], acc, 0, 0, 0);
+    return acc;
+}
+
 template <int NTT>
-__device__ __forceinline__ void b2_pw(const float* Q, const float (&a3)[MAXKS3], int KS3, int NT1, int RB,
-                                      const B2Map& mp, floatx4 (&acc)[NTT], int lane) {
-    const int li = lane & 15, lk = lane >> 4;
+__device__ __forceinline__ void b2_pw(const float* Q, const float* W3s, int F2P, int NT1, int RB, const B2Map& mp,
+                                      floatx4 (&acc)[NTT], int lane) {
 #pragma unroll
     for (int i = 0; i < NTT; ++i) {
-        acc[i] = (floatx4){0.f, 0.f, 0.f, 0.f};
         const int n = mp.n0 + mp.dn * i;
-        if (n < NT1) {
-            const float* qc = Q + lk * RB + LQW + 16 * n + li;
-#pragma unroll
-            for (int s = 0; s < MAXKS3; ++s)
-                if (s < KS3) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[s], qc[4 * s * RB], acc[i], 0, 0, 0);
-        }
+        acc[i] = n < NT1 ? b2_pw_tile(Q, W3s, F2P, mp.jt, n, RB, lane) : (floatx4){0.f, 0.f, 0.f, 0.f};
     }
 }
 
-__device__ __forceinline__ void load_a3(const Geo& g, const float* __restrict__ prm, int jt, float (&a3)[MAXKS3],
-                                        int lane) {
-    const int jj = 16 * jt + (lane & 15), lk = lane >> 4;
-#pragma unroll
-    for (int s = 0; s < MAXKS3; ++s) {
-        const int i = 4 * s + lk;
-        a3[s] = (jj < g.F2 && i < g.F2) ? prm[g.o_W3 + jj * g.F2 + i] : 0.f;
+// W3 [F2][F2] into the LDS table W3s [F2P][F2P + 1] (zero padding)
+__device__ __forceinline__ void stage_w3(const Geo& g, const float* __restrict__ prm, float* W3s, int F2P, int tid,
+                                         int nth) {
+    const int W3S = F2P + 1;
+    for (int i = tid; i < F2P * W3S; i += nth) {
+        const int jj = i / W3S, ii = i - jj * W3S;
+        W3s[i] = (jj < g.F2 && ii < g.F2) ? prm[g.o_W3 + jj * g.F2 + ii] : 0.f;
     }
 }
 
@@ -440,15 +460,15 @@ __global__ __launch_bounds__(NTB2) void k_wpass_b2(Geo g, const float* __restric
     float* D2 = sm;
     float* Q = D2 + F2P * RB;
     float* W2s = Q + F2P * RB;
-    float* ws_ = W2s + F2P * K2;
+    float* W3s = W2s + F2P * K2;
+    float* ws_ = W3s + F2P * (F2P + 1);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     for (int i = tid; i < 2 * F2P * RB; i += NTB2) sm[i] = 0.f;
     load_w2s(g, prm, W2s, F2P, tid);
+    stage_w3(g, prm, W3s, F2P, tid, NTB2);
     const B2Map mp = b2_map(NJT, wave);
-    float a3[MAXKS3];
-    load_a3(g, prm, mp.jt, a3, lane);
     float sr[4] = {0.f, 0.f, 0.f, 0.f}, sr2[4] = {0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     drain_prologue_loads();
@@ -458,7 +478,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_b2(Geo g, const float* __restric
         b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
         __syncthreads();
         floatx4 acc[NTTW];
-        b2_pw<NTTW>(Q, a3, KS3, NT1, RB, mp, acc, lane);
+        b2_pw<NTTW>(Q, W3s, F2P, NT1, RB, mp, acc, lane);
 #pragma unroll
         for (int i = 0; i < NTTW; ++i) {
             const int t = 16 * (mp.n0 + mp.dn * i) + li;
@@ -525,17 +545,18 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
     float* D2 = sm;
     float* Q = D2 + F2P * RB;
     float* W2s = Q + F2P * RB;
-    float* H = W2s + F2P * K2;
+    float* W3s = W2s + F2P * K2;
+    float* H = W3s + F2P * (F2P + 1);
     float* lgs = H + ((NF + 3) & ~3);
     float* ws_ = lgs + NWB2 * 4;
+    float* XH = ws_ + NWB2 * 2 * 16;                   // BN3-normalised r [F2P][RB] (t at LQW + t)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     for (int i = tid; i < 2 * F2P * RB; i += NTB2) sm[i] = 0.f;
     load_w2s(g, prm, W2s, F2P, tid);
+    stage_w3(g, prm, W3s, F2P, tid, NTB2);
     const B2Map mp = b2_map(NJT, wave);
-    float a3[MAXKS3];
-    load_a3(g, prm, mp.jt, a3, lane);
     float g3[4], b3[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -564,21 +585,30 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
         __syncthreads();
         b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
         __syncthreads();
-        floatx4 acc[NTTW];
-        b2_pw<NTTW>(Q, a3, KS3, NT1, RB, mp, acc, lane);
-        float mu[4], inv[4];
-        b2_bn3(coef, mp, acc, lane, mu, inv);
-        // ELU -> AvgPool(1,8) -> H (flattened index j*T2 + t/8, model.py:75)
-#pragma unroll
-        for (int i = 0; i < NTTW; ++i) {
-            const int n = mp.n0 + mp.dn * i;
-            const int t = 16 * n + li;
+        {
+            float mu[4], inv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int jj = 16 * mp.jt + 4 * lk + r;
-                float e = (n < NT1 && t < 8 * T2) ? elu_f(fmaf(g3[r], acc[i][r], b3[r])) : 0.f;
-                e = sum8_hi(e);
-                if ((lane & 7) == 7 && n < NT1 && t < 8 * T2 && jj < F2) H[jj * T2 + (t >> 3)] = e * 0.125f;
+                mu[r] = coef[CF_MU3 * CSTR + jj];
+                inv[r] = coef[CF_INV3 * CSTR + jj];
+            }
+            // per time tile: pointwise (MFMA) -> BN3 -> XH; ELU -> AvgPool(1,8) -> H (flattened
+            // index j*T2 + t/8, model.py:75)
+            for (int i = 0; i < NTTW; ++i) {
+                const int n = mp.n0 + mp.dn * i;
+                if (n >= NT1) break;
+                const floatx4 acc = b2_pw_tile(Q, W3s, F2P, mp.jt, n, RB, lane);
+                const int t = 16 * n + li;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int jj = 16 * mp.jt + 4 * lk + r;
+                    const float xh = (acc[r] - mu[r]) * inv[r];
+                    XH[jj * RB + LQW + t] = xh;
+                    float e = t < 8 * T2 ? elu_f(fmaf(g3[r], xh, b3[r])) : 0.f;
+                    e = sum8_hi(e);
+                    if ((lane & 7) == 7 && t < 8 * T2 && jj < F2) H[jj * T2 + (t >> 3)] = e * 0.125f;
+                }
             }
         }
         __syncthreads();                                   // H complete
@@ -638,18 +668,19 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
                 if (f < NF) H[f] = d * kp[u];                           // dp3 (own slots)
             }
             __syncthreads();
-            // BN3-backward sums: dz3 = dp3 / 8 * ELU'(z3)
-#pragma unroll
+            // BN3-backward sums: dz3 = dp3 / 8 * ELU'(z3) (this wave's own XH entries)
             for (int i = 0; i < NTTW; ++i) {
                 const int n = mp.n0 + mp.dn * i;
+                if (n >= NT1) break;
                 const int t = 16 * n + li;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int jj = 16 * mp.jt + 4 * lk + r;
-                    if (n < NT1 && t < 8 * T2 && jj < F2) {
-                        const float dz = H[jj * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3[r], acc[i][r], b3[r]));
+                    if (t < 8 * T2 && jj < F2) {
+                        const float xh = XH[jj * RB + LQW + t];
+                        const float dz = H[jj * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3[r], xh, b3[r]));
                         sdz[r] += dz;
-                        sdzx[r] = fmaf(dz, acc[i][r], sdzx[r]);
+                        sdzx[r] = fmaf(dz, xh, sdzx[r]);
                     }
                 }
             }
@@ -710,24 +741,18 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
     float* Q = D2 + F2P * RB;
     float* DR = Q + F2P * RB;
     float* W2s = DR + F2P * RB;
-    float* Hd = W2s + F2P * K2;
-    float* isum = sm;                                   // [2][MAXIW][NTB2] item partials (after the loop)
+    float* W3s = W2s + F2P * K2;
+    float* Hd = W3s + F2P * (F2P + 1);
+    float* IS = Hd + ((NF + 3) & ~3);                  // [2][F2 * TQ1] BN2-bwd item sums (per thread)
+    const int nit = F2 * TQ1;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     for (int i = tid; i < 3 * F2P * RB; i += NTB2) sm[i] = 0.f;
+    for (int i = tid; i < 2 * nit; i += NTB2) IS[i] = 0.f;
     load_w2s(g, prm, W2s, F2P, tid);
+    stage_w3(g, prm, W3s, F2P, tid, NTB2);
     const B2Map mp = b2_map(NJT, wave);
-    float a3[MAXKS3], a3t[MAXKS3];
-    load_a3(g, prm, mp.jt, a3, lane);
-    {   // W3^T fragments of row tile it = mp.jt: lane l holds W3[4 s + (l >> 4)][16 it + (l & 15)]
-        const int ii = 16 * mp.jt + li;
-#pragma unroll
-        for (int s = 0; s < MAXKS3; ++s) {
-            const int jj = 4 * s + lk;
-            a3t[s] = (ii < F2 && jj < F2) ? prm[g.o_W3 + jj * F2 + ii] : 0.f;
-        }
-    }
     float g3[4], b3[4], A3[4], B3[4], C3[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -751,10 +776,6 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
     // dw2 item of this thread: row o2, taps 4 kq .. 4 kq + 3
     const int o2 = tid >> 2, kq = tid & 3;
     float acc2[4] = {0.f, 0.f, 0.f, 0.f};
-    // dd2 items: (row, quad) it = tid + NTB2 m -- a fixed row per (thread, m) across trials
-    float sz1[MAXIW], sz2[MAXIW];
-#pragma unroll
-    for (int m = 0; m < MAXIW; ++m) { sz1[m] = 0.f; sz2[m] = 0.f; }
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
@@ -775,19 +796,22 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
         b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
         __syncthreads();
         {   // BN3 backward (finalize 3's batch constants): dr = A3 dz3 + B3 + C3 xh3 -> DR rows
-            floatx4 acc[NTTW];
-            b2_pw<NTTW>(Q, a3, KS3, NT1, RB, mp, acc, lane);
             float mu[4], inv[4];
-            b2_bn3(coef, mp, acc, lane, mu, inv);
 #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jj = 16 * mp.jt + 4 * lk + r;
+                mu[r] = coef[CF_MU3 * CSTR + jj];
+                inv[r] = coef[CF_INV3 * CSTR + jj];
+            }
             for (int i = 0; i < NTTW; ++i) {
                 const int n = mp.n0 + mp.dn * i;
-                if (n >= NT1) continue;
+                if (n >= NT1) break;
+                const floatx4 acc = b2_pw_tile(Q, W3s, F2P, mp.jt, n, RB, lane);
                 const int t = 16 * n + li;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int jj = 16 * mp.jt + 4 * lk + r;
-                    const float xh = acc[i][r];
+                    const float xh = (acc[r] - mu[r]) * inv[r];
                     const float dz = (t < 8 * T2 && jj < F2)
                                          ? Hd[jj * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3[r], xh, b3[r])) : 0.f;
                     const float d = (t < T1 && jj < F2) ? fmaf(A3[r], dz, fmaf(C3[r], xh, B3[r])) : 0.f;
@@ -813,26 +837,20 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
                 }
             }
         }
-        // dq[i][t] = sum_j W3[j][i] dr[j][t]: A = W3^T fragments, B = DR rows
-        floatx4 dq[NTTW];
-#pragma unroll
-        for (int i = 0; i < NTTW; ++i) {
-            dq[i] = (floatx4){0.f, 0.f, 0.f, 0.f};
-            const int n = mp.n0 + mp.dn * i;
-            if (n < NT1) {
-                const float* dc = DR + lk * RB + LQW + 16 * n + li;
-#pragma unroll
-                for (int s = 0; s < MAXKS3; ++s)
-                    if (s < KS3) dq[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a3t[s], dc[4 * s * RB], dq[i], 0, 0, 0);
-            }
-        }
         __syncthreads();                                   // every reader of q is past: dq -> Q
-#pragma unroll
+        // dq[i][t] = sum_j W3[j][i] dr[j][t]: A = W3^T fragments (W3s[4 s + lk][16 it + li]), B = DR
         for (int i = 0; i < NTTW; ++i) {
             const int n = mp.n0 + mp.dn * i;
-            if (n >= NT1) continue;
+            if (n >= NT1) break;
+            const float* dc = DR + lk * RB + LQW + 16 * n + li;
+            const float* at = W3s + lk * (F2P + 1) + 16 * mp.jt + li;
+            floatx4 dq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Q[(16 * mp.jt + 4 * lk + r) * RB + LQW + 16 * n + li] = dq[i][r];
+            for (int s = 0; s < MAXKS3; ++s)
+                if (s < KS3)
+                    dq = __builtin_amdgcn_mfma_f32_16x16x4f32(at[4 * s * (F2P + 1)], dc[4 * s * RB], dq, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Q[(16 * mp.jt + 4 * lk + r) * RB + LQW + 16 * n + li] = dq[r];
         }
         __syncthreads();
         // dw2[o][k] += sum_t dq[o][t] d2p[o][t + k - 7]
@@ -851,11 +869,9 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
         }
         // dd2[t] = sum_k w2[k] dq[t + 7 - k] -> dropout -> dp2; BN2-backward sums (E1 / E2 of pass B)
         const size_t rb = (size_t)b * F2 * T1;
-#pragma unroll
-        for (int m = 0; m < MAXIW; ++m) {
-            const int it = tid + NTB2 * m;
-            if (it >= F2 * TQ1) break;
+        for (int it = tid; it < nit; it += NTB2) {
             const int o = it / TQ1, qd = it - o * TQ1;
+            float s1 = 0.f, s2 = 0.f;
             float w[24];
             lds_window<6>(Q + o * RB + LQW + 4 * qd - 8, w);              // dq[t - 8 .. t + 15]
             float wt[K2];
@@ -870,10 +886,12 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
                     const size_t gi = rb + (size_t)o * T1 + t;
                     const float dp = a * keep_mul(g, mask2, dk0, (unsigned)gi);
                     dp2g[gi] = dp;
-                    sz1[m] = fmaf(dp * 0.25f, E1g[gi], sz1[m]);
-                    sz2[m] = fmaf(dp * 0.25f, E2g[gi], sz2[m]);
+                    s1 = fmaf(dp * 0.25f, E1g[gi], s1);
+                    s2 = fmaf(dp * 0.25f, E2g[gi], s2);
                 }
             }
+            IS[it] += s1;                                  // this thread's own slots
+            IS[nit + it] += s2;
         }
         __syncthreads();                                   // D2, Q, DR, Hd free for the next trial
     }
@@ -896,19 +914,10 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
         for (int kk = 0; kk < 4; ++kk) pub(row + F2 * F2 + o2 * K2 + 4 * kq + kk, acc2[kk]);
     }
     // item partials -> per-row sums in a fixed order (items of row o are it = o TQ1 + qd)
-#pragma unroll
-    for (int m = 0; m < MAXIW; ++m) {
-        isum[(0 * MAXIW + m) * NTB2 + tid] = sz1[m];
-        isum[(1 * MAXIW + m) * NTB2 + tid] = sz2[m];
-    }
-    __syncthreads();
     for (int q = tid; q < 2 * F2; q += NTB2) {
         const int o = q < F2 ? q : q - F2, h = q < F2 ? 0 : 1;
         float a = 0.f;
-        for (int qd = 0; qd < TQ1; ++qd) {
-            const int it = o * TQ1 + qd, m = it / NTB2, th = it - m * NTB2;
-            a += isum[(h * MAXIW + m) * NTB2 + th];
-        }
+        for (int qd = 0; qd < TQ1; ++qd) a += IS[h * nit + o * TQ1 + qd];
         pub(row + F2 * F2 + 16 * F2 + q, a);
     }
     double* dsm = (double*)sm;
@@ -936,12 +945,12 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     float* Dys = Ss + 16 * RS;
     float* DP = Dys + 16 * RS;
     float* CT = DP + ((16 * T1 + 3) & ~3);
+    float* awl = CT + 8 * 16;                          // ws fragments [KSW][64]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     for (int i = tid; i < 2 * 16 * RS; i += NTW) sm[i] = 0.f;
-    float aw[KSW];
-    load_aw_chunk(g, prm, o0, aw, lane);
+    stage_aw_chunk(g, prm, o0, awl, tid, NTW);
     const int o = o0 + wave;
     const bool row_on = wave < nrows;
     const int oo = row_on ? o : 0;
@@ -971,7 +980,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         for (int i = tid; i < ndp; i += NTW) DP[i] = dp2g[((size_t)b * F2 + o0) * T1 + i];
-        spatial_chunk(x + (size_t)b * C * T, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+        spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
         __syncthreads();                                   // s rows, dp2 rows complete
         if (row_on) {
             const float* row = Ss + wave * RS;
@@ -1117,8 +1126,10 @@ __global__ __launch_bounds__(NTW) void k_winfer(Geo g, const float* __restrict__
     float* D2 = Ss + 16 * RS;
     float* Q = D2 + F2P * RB;
     float* W2s = Q + F2P * RB;
-    float* H = W2s + F2P * K2;
+    float* W3s = W2s + F2P * K2;
+    float* H = W3s + F2P * (F2P + 1);
     float* AF = H + ((NF + 3) & ~3);                   // [F2P][4]: al, be (BN1+BN2), s3, b3 (BN3)
+    float* awl = AF + 4 * F2P;                         // ws fragments [NOC][KSW][64]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
@@ -1140,18 +1151,16 @@ __global__ __launch_bounds__(NTW) void k_winfer(Geo g, const float* __restrict__
         AF[4 * tid + 2] = s3;
         AF[4 * tid + 3] = prm[g.o_b3 + oo] - rm3[oo] * s3;
     }
+    stage_w3(g, prm, W3s, F2P, tid, NTW);
+    for (int j = 0; j < g.NOC; ++j) stage_aw_chunk(g, prm, 16 * j, awl + j * KSW * 64, tid, NTW);
     // pointwise tiles: wave w -> (row tile jt = w % NJT, time tiles n = w / NJT + (NWW / NJT) i)
     const int jt = wave % NJT, n0 = wave / NJT, dn = NWW / NJT;
-    float a3[MAXKS3];
-    load_a3(g, prm, jt, a3, lane);
     const int NO = (T + 7) >> 3;
     __syncthreads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
         const float* xb = x + (size_t)b * C * T;
         for (int j = 0; j < g.NOC; ++j) {
-            float aw[KSW];
-            load_aw_chunk(g, prm, 16 * j, aw, lane);
-            spatial_chunk(xb, aw, Ss, C, T, NT16, RS, LP, wave, lane);
+            spatial_chunk(xb, awl + j * KSW * 64, Ss, C, T, NT16, RS, LP, wave, lane);
             __syncthreads();
             const int o = 16 * j + wave;
             if (o < F2) {
@@ -1198,11 +1207,7 @@ __global__ __launch_bounds__(NTW) void k_winfer(Geo g, const float* __restrict__
         __syncthreads();
         // pointwise (MFMA), BN3 (eval), ELU, pool8 -> H
         for (int n = n0; n < NT1; n += dn) {
-            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-            const float* qc = Q + lk * RB + LQW + 16 * n + li;
-#pragma unroll
-            for (int s = 0; s < MAXKS3; ++s)
-                if (s < KS3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a3[s], qc[4 * s * RB], acc, 0, 0, 0);
+            const floatx4 acc = b2_pw_tile(Q, W3s, F2P, jt, n, RB, lane);
             const int t = 16 * n + li;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

@@ -42,7 +42,10 @@ class FoldBatch:
     modes, so replays draw fresh masks each step and graph and eager runs are bit-identical."""
 
     def __init__(self, models: list[EEGNet], seeds: list[int], lr=1e-3, betas=(0.9, 0.999),
-                 eps=1e-7, graphs=False):
+                 eps=1e-7, graphs=False, fused=None):
+        """``fused``: advance all folds with ONE launch per pass (eegnet_train_step_folds, the fold
+        index in the grid) instead of one stream per fold.  ``None`` picks it whenever it applies:
+        same model shape for every fold, F1*D <= 16, and (per epoch) the same number of trials."""
         if len(models) != len(seeds) or not models:
             raise ValueError("need one seed per model and at least one model")
         dev = models[0].flat_parameters().device
@@ -56,6 +59,11 @@ class FoldBatch:
         self.streams = [torch.cuda.Stream(device=dev) for _ in models]
         self._ws: list[dict] = [{} for _ in models]
         self._graph: list[_FoldGraph | None] = [None] * len(models)
+        same = all(m.shape == models[0].shape for m in models) and models[0].shape.F2 <= 16
+        if fused and not same:
+            raise ValueError("fused fold launches need the same EEGNet shape (F1*D <= 16) for every fold")
+        self.fused = same if fused is None else bool(fused)
+        self._fz = None                     # fused-launch state: buffers, fold tables, graph
 
     def __len__(self):
         return len(self.models)
@@ -81,6 +89,68 @@ class FoldBatch:
                            losses[j:j + 1], lr=self.lr, betas=self.betas, eps=self.eps,
                            nbt=m.flat_num_batches_tracked(), key_from_step=True)
 
+    # -- fused launches: all folds in one grid --------------------------------------------------
+    def _fused_state(self, data, batch_size):
+        X0, _ = data[0]
+        n = X0.shape[0]
+        st = self._fz
+        if st is not None and st["n"] == n and st["bs"] == batch_size and \
+                all(a is d[0] for a, d in zip(st["src"], data)):
+            return st
+        dev = X0.device
+        K = len(self.models)
+        nsteps = (n + batch_size - 1) // batch_size
+        st = {"n": n, "bs": batch_size, "src": [d[0] for d in data], "graph": None,
+              "Xp": [torch.empty_like(X) for X, _ in data], "yp": [torch.empty_like(y) for _, y in data],
+              "perm": [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(K)],
+              "losses": [torch.zeros(nsteps, dtype=torch.float32, device=dev) for _ in range(K)],
+              "tables": {}, "steps": []}
+        for j, i in enumerate(range(0, n, batch_size)):
+            B = min(batch_size, n - i)
+            st["steps"].append((i, j, B))
+            if B not in st["tables"]:
+                ents = []
+                for k, m in enumerate(self.models):
+                    a = self.adam[k]
+                    ents.append(dict(params=m.flat_parameters(), bn_buffers=m.flat_bn_buffers(),
+                                     num_batches_tracked=m.flat_num_batches_tracked(), x=st["Xp"][k],
+                                     labels=st["yp"][k], grads=a.grads, adam_state=a.state, step=a.step,
+                                     losses=st["losses"][k], ws=self._workspace(k, B), seed=self.seeds[k]))
+                st["tables"][B] = ops.fold_table(ents, dev)
+        self._fz = st
+        return st
+
+    def _fused_steps(self, st, data):
+        for k, (X, y) in enumerate(data):
+            torch.index_select(X, 0, st["perm"][k], out=st["Xp"][k])
+            torch.index_select(y, 0, st["perm"][k], out=st["yp"][k])
+        shape = self.models[0].shape
+        K = len(self.models)
+        for i, j, B in st["steps"]:
+            ops.train_step_folds(shape, B, st["tables"][B], K, row0=i, slot=j, offset=0, lr=self.lr,
+                                 betas=self.betas, eps=self.eps)
+
+    def _epoch_fused(self, data, batch_size, generators):
+        n = data[0][0].shape[0]
+        st = self._fused_state(data, batch_size)
+        for k in range(len(self.models)):
+            g = generators[k] if generators is not None else None
+            perm = epoch_permutation(n, g) if g is not None else torch.arange(n)
+            st["perm"][k].copy_(perm, non_blocking=True)
+        if st["graph"] is not None:
+            st["graph"].replay()
+        else:
+            self._fused_steps(st, data)
+            if self.graphs:                 # capture for the next epochs (tables / workspaces exist)
+                torch.cuda.synchronize()
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    self._fused_steps(st, data)
+                st["graph"] = gr
+                # the capture recorded without executing: run this epoch's work once more is NOT
+                # wanted -- the eager pass above already trained the epoch
+        return [l.sum(dtype=torch.float64) for l in st["losses"]]
+
     def epoch(self, data: list[tuple[torch.Tensor, torch.Tensor]], batch_size: int = 64,
               generators: list[torch.Generator] | None = None) -> list[torch.Tensor]:
         """One training epoch of every fold.  ``data[k] = (X_k [N_k,C,T] fp32, y_k [N_k] int64)``,
@@ -90,6 +160,8 @@ class FoldBatch:
         (the reference's running loss, model.py:150).  Nothing is synchronised."""
         if len(data) != len(self.models):
             raise ValueError("one (X, y) per fold")
+        if self.fused and all(X.shape[0] == data[0][0].shape[0] for X, _ in data):
+            return self._epoch_fused(data, batch_size, generators)
         cur = torch.cuda.current_stream()
         sums = []
         for k, (X, y) in enumerate(data):

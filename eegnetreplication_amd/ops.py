@@ -176,3 +176,29 @@ def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset:
         ctypes.c_float(eps), _ptr(loss), _ptr(logits), _ptr(ws), _stream(),
         (0 if clamp else NO_CLAMP) | (KEY_FROM_STEP if key_from_step else 0), _ptr(nbt)),
         "eegnet_train_step")
+
+
+def fold_table(entries, device) -> torch.Tensor:
+    """Device array of ``eegnet_fold`` entries (a uint8 tensor holding the packed structs).
+    ``entries``: dicts with the eegnet_fold fields as tensors (or None) and ``seed`` as an int."""
+    n = len(entries)
+    arr = (_lib.Fold * n)()
+    for i, e in enumerate(entries):
+        for name, _ in _lib.Fold._fields_[:-1]:
+            t = e.get(name)
+            setattr(arr[i], name, 0 if t is None else t.data_ptr())
+        arr[i].seed = int(e["seed"]) & ((1 << 64) - 1)
+    raw = bytes(arr)
+    return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+
+
+def train_step_folds(shape: Shape, B: int, table: torch.Tensor, nfolds: int, row0: int, slot: int,
+                     offset: int = 0, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, p: float | None = None):
+    """eegnet_train_step_folds: one fused step of ``nfolds`` independent models in one launch per
+    pass (fold index = grid y).  ``table`` from fold_table(); every fold trains on rows
+    [row0, row0 + B) of its own x / labels and writes its loss to losses[slot]."""
+    d = shape.dims(B, p)
+    _lib.check(_lib.load().eegnet_train_step_folds(
+        ctypes.byref(d), ctypes.c_int(nfolds), _ptr(table), ctypes.c_int64(row0), ctypes.c_int64(slot),
+        ctypes.c_uint64(offset), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
+        ctypes.c_float(eps), _stream()), "eegnet_train_step_folds")

@@ -128,6 +128,34 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
                       float eps, float* loss, float* logits, void* ws, void* stream, int flags,
                       int64_t* num_batches_tracked);
 
+/* One model (fold) of a fold-indexed train step: everything eegnet_train_step takes per model.
+ * Every pointer is a device pointer; an array of these lives in DEVICE memory. */
+typedef struct eegnet_fold {
+    float* params;                  /* flat parameters (named_parameters order)                   */
+    float* bn_buffers;              /* rm1 rv1 rm2 rv2 rm3 rv3                                    */
+    int64_t* num_batches_tracked;   /* int64[3] or NULL                                           */
+    const float* x;                 /* this fold's epoch data [N, C, T], rows already shuffled    */
+    const int64_t* labels;          /* [N]                                                        */
+    float* grads;                   /* flat gradients (written)                                   */
+    float* adam_state;              /* [exp_avg | exp_avg_sq]                                     */
+    int32_t* step;                  /* Adam step counter (device int32)                           */
+    float* losses;                  /* per-batch loss slots (NULL: not written)                   */
+    void* ws;                       /* workspace of eegnet_workspace_bytes(dims), zeroed once     */
+    uint64_t seed;                  /* dropout key seed: key = mix(seed, offset + *step)          */
+} eegnet_fold;
+
+/* The hot-loop iteration of eegnet_train_step (forward + CE + backward + clamps + Adam) for
+ * `nfolds` independent models in ONE launch per pass: the fold index is the grid's y dimension,
+ * each fold keeps its own parameters, BN buffers, Adam state, workspace and reductions.  Replaces
+ * the per-fold loops of train.py:50-140 (within-subject, 36 runs) and train.py:182-290
+ * (cross-subject, 90 runs) at batch 64 (train.py:87,229), where one model's step cannot fill the
+ * GPU.  All folds train on batch [row0, row0 + dims.B) of their own x / labels; the loss goes to
+ * losses[slot].  Dropout keys follow each fold's device step (EEGNET_KEY_FROM_STEP semantics with
+ * `offset`), so a captured graph draws fresh masks on every replay.  F1*D <= 16 only. */
+int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fold* folds, int64_t row0,
+                            int64_t slot, uint64_t offset, float lr, float beta1, float beta2, float eps,
+                            void* stream);
+
 /* Optional per-kernel device timing for benchmarks: `on` is a bitmask of kernel ids (bit i = the
  * i-th name eegnet_profile_collect reports: k_pass_a, k_pass_b, k_pass_c, k_pass_d, k_pass_e,
  * k_adam, k_infer, memset_tickets, k_infer_bf16, k_wpass_a, k_wpass_b, k_wpass_b2, k_wpass_c,

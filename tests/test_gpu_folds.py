@@ -186,3 +186,31 @@ def test_graph_fold_edge_sizes(sizes):
             for a, b in zip(_state(eager, k), _state(graph, k)):
                 assert torch.equal(a, b)
             assert np.isfinite(float(sg[k]))
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_fold_launch_equals_per_fold_streams(graphs):
+    """eegnet_train_step_folds (all folds in one launch per pass, fold = grid y) against the same
+    folds advanced on one stream each: identical parameters, BN buffers, counters, Adam state and
+    loss sums, epoch after epoch (equal-size folds, a short last batch, p = 0.5)."""
+    from eegnetreplication_amd import FoldBatch
+    dev = _dev()
+    K, n = 5, 150
+    seeds = [40 + k for k in range(K)]
+    data = [_data(n, 500 + k, dev) for k in range(K)]
+    models = _models(K, 0.5, dev)
+    twins = [_clone(m, 0.5, dev) for m in models]
+    fused = FoldBatch(models, seeds, graphs=graphs, fused=True)
+    split = FoldBatch(twins, seeds, graphs=graphs, fused=False)
+    gf = [torch.Generator().manual_seed(s) for s in seeds]
+    gs = [torch.Generator().manual_seed(s) for s in seeds]
+    for e in range(3):
+        sf = fused.epoch(data, 64, gf)
+        ss = split.epoch(data, 64, gs)
+        torch.cuda.synchronize()
+        for k in range(K):
+            assert torch.equal(sf[k], ss[k]), f"epoch {e} fold {k}: loss sums differ"
+            for a, b in zip(_state(fused, k), _state(split, k)):
+                assert torch.equal(a, b), f"epoch {e} fold {k}: fused launch differs from per-fold streams"
+    assert fused._fz is not None and (fused._fz["graph"] is not None) == graphs
+    assert int(fused.adam[0].step.item()) == 3 * 3
