@@ -65,7 +65,7 @@ struct Geo {
     unsigned long long* trace;
     // F2 > 16 (eegnet_wide.hip): o-chunks of 16 rows, Gram electrode slice per chunk, block-2 rows
     // padded to F2P (32 / 64), block-2 row stride; LDS (floats) of the wide kernels
-    int wide, NOC, CPC, F2P, RB;
+    int wide, NOC, CPC, F2P, RB, gridB2;
     int ldsWA, ldsWB, ldsWB2, ldsWC, ldsWD, ldsWE, ldsWI;
 };
 

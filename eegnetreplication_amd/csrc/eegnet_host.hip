@@ -44,6 +44,28 @@ static unsigned long long* g_trace_buf = nullptr;     // eegnet_trace_enable
 
 static int make_geo_wide(Geo* g, bool launch);
 
+// LDS (floats) of the whole-trial block-2 passes (eegnet_wide.hip k_wpass_b2 / c / d) at nw waves
+static void b2_lds(Geo* g, int nw) {
+    auto tailw = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + fin); };
+    const int nf4 = (g->NF + 3) / 4 * 4;
+    const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables
+    const int TQ1 = (g->T1 + 3) / 4;
+    g->ldsWB2 = std::max(b2 + nw * 2 * 16, tailw(g->nB, 0));
+    g->ldsWC = std::max(b2 + nf4 + nw * 4 + nw * 2 * 16 + g->F2P * g->RB, tailw(g->nC, 0));
+    g->ldsWD = std::max(b2 + g->F2P * g->RB + nf4 + 2 * g->F2 * TQ1, tailw(g->nD, 0));
+}
+
+// Block-2 passes C / D of the F2 <= 16 step: one trial per wave (k_pass_c / k_pass_d, the better
+// choice at large batches: B = 4096 runs them in 32 / 50 us against 68 / 83 us) or whole-trial
+// 256-thread workgroups (the wide path's k_wpass_c / k_wpass_d: more workgroups, so the better
+// choice at small per-launch grids, e.g. batch 64 and fold-indexed launches).  EEGNET_B2=0/1 forces.
+static bool use_b2_narrow(const Geo& g) {
+    static int v = -2;
+    if (v == -2) { const char* e = getenv("EEGNET_B2"); v = e ? (e[0] == '1' ? 1 : 0) : -1; }
+    if (v >= 0) return v == 1;
+    return g.gridB2 < 4 * device_cus() / 2;     // small batches (e.g. the protocols' 64): more workgroups
+}
+
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     if (!d) return fail(EEGNET_EINVAL, "dims is NULL");
     memset(g, 0, sizeof(*g));
@@ -116,6 +138,10 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->ldsE = std::max(g->ldsE, tail(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->o_g2)));
     g->wide = g->F2 > F2MAX ? 1 : 0;
     if (g->wide) return make_geo_wide(g, launch);
+    g->F2P = 16;
+    g->RB = rb_stride(g->T1);
+    b2_lds(g, 4);
+    g->gridB2 = std::min(g->B, 4 * device_cus());
     if (launch) {
         if (g->C * g->T > NTH * MAXPF)
             return fail(EEGNET_EINVAL, "C*T = %d exceeds the %d-float prefetch of one trial", g->C * g->T,
@@ -154,13 +180,12 @@ static int make_geo_wide(Geo* g, bool launch) {
                         tailw(g->nA, std::max(NTH, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C))));
     g->ldsWB = 16 * g->RS + awl;
     const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables
-    const int TQ1 = (g->T1 + 3) / 4;
-    g->ldsWB2 = std::max(b2 + NWB2 * 2 * 16, tailw(g->nB, 0));
-    g->ldsWC = std::max(b2 + nf4 + NWB2 * 4 + NWB2 * 2 * 16 + g->F2P * g->RB, tailw(g->nC, 0));
-    g->ldsWD = std::max(b2 + g->F2P * g->RB + nf4 + 2 * g->F2 * TQ1, tailw(g->nD, 0));
+    b2_lds(g, NWB2);
+    g->gridB2 = g->grid;
     g->ldsWE = std::max(std::max(2 * 16 * g->RS + rup(16 * g->T1, 4) + 8 * 16 + awl, NWW * 256 + 16 * (g->K1 + 2)),
                         tailw(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->o_g2)));
     g->ldsWI = 16 * g->RS + b2 + nf4 + 4 * g->F2P + g->NOC * awl;
+    (void)nf4;
     if (!launch) return 0;
     if (g->C > 4 * KSW) return fail(EEGNET_EINVAL, "C = %d > %d", g->C, 4 * KSW);
     if (g->T1 > 16 * NTTW * (NWB2 / 4)) return fail(EEGNET_EINVAL, "T/4 = %d > %d", g->T1, 16 * NTTW * (NWB2 / 4));
@@ -180,8 +205,8 @@ static WsLayout make_layout(const Geo& g) {
     L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
     L.partA = take((size_t)g.gridS * g.nA * 4);
     L.partB = take((size_t)std::max(g.gridS, g.grid) * g.nB * 4);
-    L.partC = take((size_t)g.grid * g.nC * 4);
-    L.partD = take((size_t)g.grid * g.nD * 4);
+    L.partC = take((size_t)std::max(g.grid, g.gridB2) * g.nC * 4);
+    L.partD = take((size_t)std::max(g.grid, g.gridB2) * g.nD * 4);
     L.partE = take((size_t)g.gridS * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
     L.sums = take((size_t)nmax * 8 * NGRPMAX);
@@ -268,7 +293,9 @@ static void ensure_attrs() {
     if (g_attr_done) return;
     set_attrs_wide<32>();
     set_attrs_wide<64>();
-    for (const void* f : {(const void*)k_wpass_b2, (const void*)k_wpass_c, (const void*)k_wpass_d})
+    for (const void* f : {(const void*)k_wpass_b2<NTB2>, (const void*)k_wpass_c<NTB2>, (const void*)k_wpass_d<NTB2>,
+                          (const void*)k_wpass_c<256>, (const void*)k_wpass_d<256>,
+                          (const void*)k_wpass_c<256, true>, (const void*)k_wpass_d<256, true>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
                           (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>,
@@ -318,7 +345,7 @@ static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const flo
     { PROF(KID_WB); hipLaunchKernelGGL((k_wpass_b<K1>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g, params,
                                       (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2),
                                       (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
-    { PROF(KID_WB2); hipLaunchKernelGGL(k_wpass_b2, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
+    { PROF(KID_WB2); hipLaunchKernelGGL(k_wpass_b2<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
                                       (const float*)(ws + L.d2), (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
     return 0;
 }
@@ -337,12 +364,12 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
         fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
     }
-    { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
+    { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
                                       (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
-                                      (float*)(ws + L.partC), c_mode, fc); } LAUNCH_CHECK("k_wpass_c(bwd)");
-    { PROF(KID_WD); hipLaunchKernelGGL(k_wpass_d, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
+                                      (float*)(ws + L.partC), c_mode, fc, FoldCall{}); } LAUNCH_CHECK("k_wpass_c(bwd)");
+    { PROF(KID_WD); hipLaunchKernelGGL(k_wpass_d<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
                                       (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
-                                      m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd); }
+                                      m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
     LAUNCH_CHECK("k_wpass_d");
     { PROF(KID_WE); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
                                       (const float*)params, coef, x, (const float*)(ws + L.dp2),
@@ -399,6 +426,25 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     else hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid, nf), dim3(64 * g.nwC), g.ldsC * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
                        (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc)
+    if (use_b2_narrow(g)) {
+        { PROF(KID_C);
+          if (fc.folds) hipLaunchKernelGGL((k_wpass_c<256, true>), dim3(g.gridB2, nf), dim3(256), g.ldsWC * 4, s, g,
+                                           params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits,
+                                           (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc);
+          else hipLaunchKernelGGL((k_wpass_c<256>), dim3(g.gridB2), dim3(256), g.ldsWC * 4, s, g, params, coef,
+                                  (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
+                                  (float*)(ws + L.partC), c_mode, fcC, fc);
+        } LAUNCH_CHECK("k_wpass_c<256>");
+        { PROF(KID_D);
+          if (fc.folds) hipLaunchKernelGGL((k_wpass_d<256, true>), dim3(g.gridB2, nf), dim3(256), g.ldsWD * 4, s, g,
+                                           params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1),
+                                           (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2),
+                                           (float*)(ws + L.partD), fd, fc);
+          else hipLaunchKernelGGL((k_wpass_d<256>), dim3(g.gridB2), dim3(256), g.ldsWD * 4, s, g, params, coef,
+                                  (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
+                                  m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, fc);
+        } LAUNCH_CHECK("k_wpass_d<256>");
+    } else {
     { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
     } LAUNCH_CHECK("k_pass_c(bwd)");
 #define LAUNCH_D(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, true>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
@@ -411,6 +457,7 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        (float*)(ws + L.partD), fd, fc)
     { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
     } LAUNCH_CHECK("k_pass_d");
+    }
 #define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
                        g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc); \
     else hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
@@ -531,10 +578,10 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     FinArgs none;
     memset(&none, 0, sizeof(none));
     if (g.wide) {
-        { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params,
+        { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params,
                                           (const float*)(w + L.coef), (const float*)(w + L.d2), mask3,
                                           (const float*)nullptr, (const int64_t*)nullptr, logits, (float*)nullptr,
-                                          (float*)nullptr, (int)PC_LOGITS, none); }
+                                          (float*)nullptr, (int)PC_LOGITS, none, FoldCall{}); }
         LAUNCH_CHECK("k_wpass_c(fwd)");
         return 0;
     }
@@ -687,6 +734,13 @@ int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fo
     set_key(&g, 0, offset);                           // the keep threshold (keys come per fold)
     ensure_attrs();
     const WsLayout L = make_layout(g);
+    // the folds share the chip: per fold, the workgroups of a full-chip grid divided by nfolds, so
+    // each workgroup runs several trials (its prologue and the reduction tail are per workgroup)
+    // and all folds are resident at once.  Fewer partial rows than the workspace holds: fine.
+    const int cus = device_cus();
+    g.gridS = std::max(1, std::min(g.B, WGPC * cus / nfolds));
+    g.grid = std::max(1, std::min(g.B, cus / nfolds));
+    g.gridB2 = std::max(1, std::min(g.B, 4 * cus / nfolds));
     FoldCall fc;
     memset(&fc, 0, sizeof(fc));
     fc.folds = folds;

@@ -352,27 +352,27 @@ __global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict_
 struct B2Map {
     int jt, n0, dn;
 };
-__device__ __forceinline__ B2Map b2_map(int NJT, int wave) {
+__device__ __forceinline__ B2Map b2_map(int NJT, int wave, int nw) {
     B2Map m;
     m.jt = wave % NJT;
     m.n0 = wave / NJT;
-    m.dn = NWB2 / NJT;
+    m.dn = nw / NJT;
     return m;
 }
 
 // stage trial b's [F2][T1] rows of a global plane into padded LDS rows [F2P][RB] (pads untouched)
 __device__ __forceinline__ void b2_stage(const float* __restrict__ src, int F2, int T1, int RB, float* dst,
-                                         int tid) {
+                                         int tid, int nth) {
     const int n = F2 * T1;
     if ((T1 & 3) == 0) {
         const int TQ1 = T1 >> 2;
-        for (int i = tid; i < n / 4; i += NTB2) {
+        for (int i = tid; i < n / 4; i += nth) {
             const int o = i / TQ1, q = i - o * TQ1;
             const float4 v = reinterpret_cast<const float4*>(src)[i];
             lds_st4(dst + o * RB + LQW + 4 * q, (floatx4){v.x, v.y, v.z, v.w});
         }
     } else {
-        for (int i = tid; i < n; i += NTB2) {
+        for (int i = tid; i < n; i += nth) {
             const int o = i / T1, t = i - o * T1;
             dst[o * RB + LQW + t] = src[i];
         }
@@ -382,9 +382,9 @@ __device__ __forceinline__ void b2_stage(const float* __restrict__ src, int F2, 
 // q[o][t] = sum_k w2[o][k] d2[o][t + k - 7] (model.py:54-61, 'same', pad 7 | 8) for every row and
 // 4-sample quad: windows of 24 floats from the padded rows (start t - 8), taps from an LDS table
 __device__ __forceinline__ void b2_dw16(const float* D2, const float* W2s, float* Q, int F2, int T1, int RB,
-                                        int tid) {
+                                        int tid, int nth) {
     const int TQ1 = (T1 + 3) >> 2;
-    for (int it = tid; it < F2 * TQ1; it += NTB2) {
+    for (int it = tid; it < F2 * TQ1; it += nth) {
         const int o = it / TQ1, qd = it - o * TQ1;
         float w[24];
         lds_window<6>(D2 + o * RB + LQW + 4 * qd - 8, w);
@@ -439,8 +439,9 @@ __device__ __forceinline__ void stage_w3(const Geo& g, const float* __restrict__
 }
 
 // w2 taps [F2P][16] (zero rows beyond F2)
-__device__ __forceinline__ void load_w2s(const Geo& g, const float* __restrict__ prm, float* W2s, int F2P, int tid) {
-    for (int i = tid; i < F2P * K2; i += NTB2) W2s[i] = i < g.F2 * K2 ? prm[g.o_w2 + i] : 0.f;
+__device__ __forceinline__ void load_w2s(const Geo& g, const float* __restrict__ prm, float* W2s, int F2P, int tid,
+                                         int nth) {
+    for (int i = tid; i < F2P * K2; i += nth) W2s[i] = i < g.F2 * K2 ? prm[g.o_w2 + i] : 0.f;
 }
 
 // time tiles per wave of the block-2 MFMA loops: NT1 = ceil(T1 / 16) <= 16 (T <= 1024) over
@@ -451,10 +452,11 @@ constexpr int NTTW = 8;
 // Wide pass B2: BN3 (model.py:71) batch statistics.  Partial row [Sr F2][Sr2 F2].
 // LDS: D2 [F2P][RB] | Q [F2P][RB] | W2s [F2P][16] | wave sums [NWB2][2][16]
 // ================================================================================================
-__global__ __launch_bounds__(NTB2) void k_wpass_b2(Geo g, const float* __restrict__ prm,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_wpass_b2(Geo g, const float* __restrict__ prm,
                                                    const float* __restrict__ d2g, float* __restrict__ part,
                                                    FinArgs fa) {
-    const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, RB = g.RB, NJT = F2P >> 4, KS3 = F2P >> 2;
+    const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, RB = g.RB, NJT = F2P >> 4;
     const int NT1 = (T1 + 15) >> 4;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2 = sm;
@@ -465,17 +467,17 @@ __global__ __launch_bounds__(NTB2) void k_wpass_b2(Geo g, const float* __restric
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    for (int i = tid; i < 2 * F2P * RB; i += NTB2) sm[i] = 0.f;
-    load_w2s(g, prm, W2s, F2P, tid);
-    stage_w3(g, prm, W3s, F2P, tid, NTB2);
-    const B2Map mp = b2_map(NJT, wave);
+    for (int i = tid; i < 2 * F2P * RB; i += NT) sm[i] = 0.f;
+    load_w2s(g, prm, W2s, F2P, tid, NT);
+    stage_w3(g, prm, W3s, F2P, tid, NT);
+    const B2Map mp = b2_map(NJT, wave, NT / 64);
     float sr[4] = {0.f, 0.f, 0.f, 0.f}, sr2[4] = {0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid);
+        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid, NT);
         __syncthreads();
-        b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
+        b2_dw16(D2, W2s, Q, F2, T1, RB, tid, NT);
         __syncthreads();
         floatx4 acc[NTTW];
         b2_pw<NTTW>(Q, W3s, F2P, NT1, RB, mp, acc, lane);
@@ -502,10 +504,10 @@ __global__ __launch_bounds__(NTB2) void k_wpass_b2(Geo g, const float* __restric
     }
     __syncthreads();
     float* row = part + (size_t)blockIdx.x * g.nB;
-    for (int q = tid; q < 2 * F2; q += NTB2) {
+    for (int q = tid; q < 2 * F2; q += NT) {
         const int o = q < F2 ? q : q - F2, h = q < F2 ? 0 : 1, jt = o >> 4;
         float a = 0.f;
-        for (int w = jt; w < NWB2; w += NJT) a += ws_[(w * 2 + h) * 16 + (o & 15)];
+        for (int w = jt; w < (NT / 64); w += NJT) a += ws_[(w * 2 + h) * 16 + (o & 15)];
         pub(row + q, a);
     }
     double* dsm = (double*)sm;
@@ -531,16 +533,32 @@ __device__ __forceinline__ void b2_bn3(const float* coef, const B2Map& mp, float
 // ================================================================================================
 // Wide pass C: head (model.py:71-84).  logits, and (PC_BWD) CE, classifier grads, BN3-bwd sums.
 // Partial row [dWfc 4*NF][dbfc 4][Sdz3 F2][Sdz3x F2][loss].
-// LDS: D2 | Q | W2s | H [NF] (features, then their gradients) | class partials [NWB2][4] | sums
+// LDS: D2 | Q | W2s | H [NF] (features, then their gradients) | class partials [(NT / 64)][4] | sums
 // ================================================================================================
-__global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict__ prm, const float* coef,
+template <int NT, bool FOLD = false>
+__global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ d2g, const uint8_t* __restrict__ mask3,
                                                   const float* __restrict__ dlin, const int64_t* __restrict__ labels,
                                                   float* __restrict__ logits, float* __restrict__ dlout,
-                                                  float* __restrict__ part, int mode, FinArgs fa) {
+                                                  float* __restrict__ part, int mode, FinArgs fa, FoldCall fc) {
     const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, T2 = g.T2, NF = g.NF, RB = g.RB;
-    const int NJT = F2P >> 4, KS3 = F2P >> 2, NT1 = (T1 + 15) >> 4;
-    const unsigned dk1 = drop_key(g, 1);
+    const int NJT = F2P >> 4, NT1 = (T1 + 15) >> 4;
+    unsigned dk1;
+    if (FOLD) {                                        // fold-indexed launch: this fold's pointers
+        const eegnet_fold& f = fc.folds[blockIdx.y];
+        char* ws = (char*)f.ws;
+        prm = f.params;
+        coef = (const float*)(ws + fc.off.coef);
+        d2g = (const float*)(ws + fc.off.d2);
+        mask3 = nullptr; dlin = nullptr; logits = nullptr;
+        labels = f.labels + fc.row0;
+        dlout = (float*)(ws + fc.off.dl);
+        part = (float*)(ws + fc.off.partC);
+        fa = fold_fin(fc, f, TK_C, 0, 1, false, false, g.nparam);
+        dk1 = fold_drop_key(fc, f, 1);
+    } else {
+        dk1 = drop_key(g, 1);
+    }
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2 = sm;
     float* Q = D2 + F2P * RB;
@@ -548,15 +566,15 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
     float* W3s = W2s + F2P * K2;
     float* H = W3s + F2P * (F2P + 1);
     float* lgs = H + ((NF + 3) & ~3);
-    float* ws_ = lgs + NWB2 * 4;
-    float* XH = ws_ + NWB2 * 2 * 16;                   // BN3-normalised r [F2P][RB] (t at LQW + t)
+    float* ws_ = lgs + (NT / 64) * 4;
+    float* XH = ws_ + (NT / 64) * 2 * 16;                   // BN3-normalised r [F2P][RB] (t at LQW + t)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    for (int i = tid; i < 2 * F2P * RB; i += NTB2) sm[i] = 0.f;
-    load_w2s(g, prm, W2s, F2P, tid);
-    stage_w3(g, prm, W3s, F2P, tid, NTB2);
-    const B2Map mp = b2_map(NJT, wave);
+    for (int i = tid; i < 2 * F2P * RB; i += NT) sm[i] = 0.f;
+    load_w2s(g, prm, W2s, F2P, tid, NT);
+    stage_w3(g, prm, W3s, F2P, tid, NT);
+    const B2Map mp = b2_map(NJT, wave, NT / 64);
     float g3[4], b3[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -568,7 +586,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
     for (int n = 0; n < NCLS; ++n)
 #pragma unroll
         for (int u = 0; u < MAXNFW; ++u) {
-            const int f = tid + NTB2 * u;
+            const int f = tid + NT * u;
             wf[n][u] = f < NF ? prm[g.o_Wfc + n * NF + f] : 0.f;
             wacc[n][u] = 0.f;
         }
@@ -581,9 +599,9 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid);
+        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid, NT);
         __syncthreads();
-        b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
+        b2_dw16(D2, W2s, Q, F2, T1, RB, tid, NT);
         __syncthreads();
         {
             float mu[4], inv[4];
@@ -616,7 +634,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
         float lg[NCLS] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < MAXNFW; ++u) {
-            const int f = tid + NTB2 * u;
+            const int f = tid + NT * u;
             kp[u] = f < NF ? keep_mul(g, mask3, dk1, (unsigned)(b * NF + f)) : 0.f;
             hv[u] = f < NF ? H[f] * kp[u] : 0.f;                       // dropout (model.py:74)
 #pragma unroll
@@ -629,7 +647,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
 #pragma unroll
         for (int n = 0; n < NCLS; ++n) {
             float a = 0.f;
-            for (int w = 0; w < NWB2; ++w) a += lgs[w * 4 + n];
+            for (int w = 0; w < (NT / 64); ++w) a += lgs[w * 4 + n];
             L[n] = a + bfc[n];
         }
         if ((mode & PC_LOGITS) && tid < NCLS)
@@ -658,7 +676,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
                 for (int n = 0; n < NCLS; ++n) bacc[n] += dl[n];
 #pragma unroll
             for (int u = 0; u < MAXNFW; ++u) {
-                const int f = tid + NTB2 * u;
+                const int f = tid + NT * u;
                 float d = 0.f;
 #pragma unroll
                 for (int n = 0; n < NCLS; ++n) {
@@ -693,7 +711,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
     for (int n = 0; n < NCLS; ++n)
 #pragma unroll
         for (int u = 0; u < MAXNFW; ++u) {
-            const int f = tid + NTB2 * u;
+            const int f = tid + NT * u;
             if (f < NF) pub(row + n * NF + f, wacc[n][u]);
         }
     float v[8] = {sdz[0], sdz[1], sdz[2], sdz[3], sdzx[0], sdzx[1], sdzx[2], sdzx[3]};
@@ -707,10 +725,10 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
         }
     }
     __syncthreads();
-    for (int q = tid; q < 2 * F2; q += NTB2) {
+    for (int q = tid; q < 2 * F2; q += NT) {
         const int o = q < F2 ? q : q - F2, h = q < F2 ? 0 : 1, jt = o >> 4;
         float a = 0.f;
-        for (int w = jt; w < NWB2; w += NJT) a += ws_[(w * 2 + h) * 16 + (o & 15)];
+        for (int w = jt; w < (NT / 64); w += NJT) a += ws_[(w * 2 + h) * 16 + (o & 15)];
         pub(row + NCLS * NF + NCLS + q, a);
     }
     if (tid == 0) {
@@ -728,14 +746,34 @@ __global__ __launch_bounds__(NTB2) void k_wpass_c(Geo g, const float* __restrict
 // [Sdz2x F2].
 // LDS: D2 [F2P][RB] | Q [F2P][RB] (q, then dq) | DR [F2P][RB] | W2s | Hd [NF] | item sums
 // ================================================================================================
-__global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict__ prm, const float* coef,
+template <int NT, bool FOLD = false>
+__global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ d2g, const float* __restrict__ E1g,
                                                   const float* __restrict__ E2g, const uint8_t* __restrict__ mask2,
                                                   const uint8_t* __restrict__ mask3, const float* __restrict__ dl,
-                                                  float* __restrict__ dp2g, float* __restrict__ part, FinArgs fa) {
+                                                  float* __restrict__ dp2g, float* __restrict__ part, FinArgs fa,
+                                                  FoldCall fc) {
     const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, T2 = g.T2, NF = g.NF, RB = g.RB;
     const int NJT = F2P >> 4, KS3 = F2P >> 2, NT1 = (T1 + 15) >> 4, TQ1 = (T1 + 3) >> 2;
-    const unsigned dk0 = drop_key(g, 0), dk1 = drop_key(g, 1);
+    unsigned dk0, dk1;
+    if (FOLD) {
+        const eegnet_fold& f = fc.folds[blockIdx.y];
+        char* ws = (char*)f.ws;
+        prm = f.params;
+        coef = (const float*)(ws + fc.off.coef);
+        d2g = (const float*)(ws + fc.off.d2);
+        E1g = (const float*)(ws + fc.off.E1); E2g = (const float*)(ws + fc.off.E2);
+        mask2 = nullptr; mask3 = nullptr;
+        dl = (const float*)(ws + fc.off.dl);
+        dp2g = (float*)(ws + fc.off.dp2);
+        part = (float*)(ws + fc.off.partD);
+        fa = fold_fin(fc, f, TK_D, 0, 0, false, false, g.nparam);
+        dk0 = fold_drop_key(fc, f, 0);
+        dk1 = fold_drop_key(fc, f, 1);
+    } else {
+        dk0 = drop_key(g, 0);
+        dk1 = drop_key(g, 1);
+    }
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2 = sm;
     float* Q = D2 + F2P * RB;
@@ -748,11 +786,11 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    for (int i = tid; i < 3 * F2P * RB; i += NTB2) sm[i] = 0.f;
-    for (int i = tid; i < 2 * nit; i += NTB2) IS[i] = 0.f;
-    load_w2s(g, prm, W2s, F2P, tid);
-    stage_w3(g, prm, W3s, F2P, tid, NTB2);
-    const B2Map mp = b2_map(NJT, wave);
+    for (int i = tid; i < 3 * F2P * RB; i += NT) sm[i] = 0.f;
+    for (int i = tid; i < 2 * nit; i += NT) IS[i] = 0.f;
+    load_w2s(g, prm, W2s, F2P, tid, NT);
+    stage_w3(g, prm, W3s, F2P, tid, NT);
+    const B2Map mp = b2_map(NJT, wave, NT / 64);
     float g3[4], b3[4], A3[4], B3[4], C3[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -765,11 +803,11 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
     for (int n = 0; n < NCLS; ++n)
 #pragma unroll
         for (int u = 0; u < MAXNFW; ++u) {
-            const int f = tid + NTB2 * u;
+            const int f = tid + NT * u;
             wf[n][u] = f < NF ? prm[g.o_Wfc + n * NF + f] : 0.f;
         }
-    // dW3 tiles of this wave: (jt, it) = q / NJT, q % NJT for q = wave + NWB2 m
-    constexpr int MW3 = 2;                              // NJT^2 / NWB2 <= 2
+    // dW3 tiles of this wave: (jt, it) = q / NJT, q % NJT for q = wave + (NT / 64) m
+    constexpr int MW3 = 16 / (NT / 64);                 // dW3 tiles per wave: NJT^2 <= 16
     floatx4 accW[MW3];
 #pragma unroll
     for (int m = 0; m < MW3; ++m) accW[m] = (floatx4){0.f, 0.f, 0.f, 0.f};
@@ -782,18 +820,18 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
         float dlv[NCLS];
 #pragma unroll
         for (int n = 0; n < NCLS; ++n) dlv[n] = dl[(size_t)b * NCLS + n];
-        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid);
+        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid, NT);
         // dh -> dropout -> dp3 (flattened) into Hd
 #pragma unroll
         for (int u = 0; u < MAXNFW; ++u) {
-            const int f = tid + NTB2 * u;
+            const int f = tid + NT * u;
             float d = 0.f;
 #pragma unroll
             for (int n = 0; n < NCLS; ++n) d = fmaf(dlv[n], wf[n][u], d);
             if (f < NF) Hd[f] = d * keep_mul(g, mask3, dk1, (unsigned)(b * NF + f));
         }
         __syncthreads();
-        b2_dw16(D2, W2s, Q, F2, T1, RB, tid);
+        b2_dw16(D2, W2s, Q, F2, T1, RB, tid, NT);
         __syncthreads();
         {   // BN3 backward (finalize 3's batch constants): dr = A3 dz3 + B3 + C3 xh3 -> DR rows
             float mu[4], inv[4];
@@ -823,7 +861,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
         // dW3[j][i] += sum_t dr[j][t] q[i][t] (float4 k-permuted operands; model.py:62-69 weight grad)
 #pragma unroll
         for (int m = 0; m < MW3; ++m) {
-            const int q = wave + NWB2 * m;
+            const int q = wave + (NT / 64) * m;
             if (q < NJT * NJT) {
                 const int jt = q / NJT, it = q - jt * NJT;
                 const float* ar = DR + (16 * jt + li) * RB + LQW + 4 * lk;
@@ -869,7 +907,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
         }
         // dd2[t] = sum_k w2[k] dq[t + 7 - k] -> dropout -> dp2; BN2-backward sums (E1 / E2 of pass B)
         const size_t rb = (size_t)b * F2 * T1;
-        for (int it = tid; it < nit; it += NTB2) {
+        for (int it = tid; it < nit; it += NT) {
             const int o = it / TQ1, qd = it - o * TQ1;
             float s1 = 0.f, s2 = 0.f;
             float w[24];
@@ -899,7 +937,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
     float* row = part + (size_t)blockIdx.x * g.nD;
 #pragma unroll
     for (int m = 0; m < MW3; ++m) {
-        const int q = wave + NWB2 * m;
+        const int q = wave + (NT / 64) * m;
         if (q < NJT * NJT) {
             const int jt = q / NJT, it = q - jt * NJT;
 #pragma unroll
@@ -914,7 +952,7 @@ __global__ __launch_bounds__(NTB2) void k_wpass_d(Geo g, const float* __restrict
         for (int kk = 0; kk < 4; ++kk) pub(row + F2 * F2 + o2 * K2 + 4 * kq + kk, acc2[kk]);
     }
     // item partials -> per-row sums in a fixed order (items of row o are it = o TQ1 + qd)
-    for (int q = tid; q < 2 * F2; q += NTB2) {
+    for (int q = tid; q < 2 * F2; q += NT) {
         const int o = q < F2 ? q : q - F2, h = q < F2 ? 0 : 1;
         float a = 0.f;
         for (int qd = 0; qd < TQ1; ++qd) a += IS[h * nit + o * TQ1 + qd];
