@@ -100,6 +100,12 @@ class EEGNet(nn.Module):
                 nflat[i:i + 1].copy_(bn.num_batches_tracked.reshape(1))
                 bn.num_batches_tracked = nflat[i:i + 1].view(())
         self._nbt_flat = nflat
+        # the tensors _flat_ok checks, gathered once (a module-tree walk per call costs ~25 us of
+        # host time, the whole budget of a batch-64 step)
+        self._plist = params
+        self._blist = [t for bn in self._bns() for t in (bn.running_mean, bn.running_var)]
+        self._nlist = [bn.num_batches_tracked for bn in self._bns()]
+        self._shape_cache = None
 
     def _apply(self, fn, recurse=True):
         super()._apply(fn, recurse)
@@ -108,22 +114,28 @@ class EEGNet(nn.Module):
         return self
 
     def _flat_ok(self) -> bool:
+        """Every parameter / BN buffer still a view of the flat buffers (a caller may rebind
+        ``p.data`` or a buffer)."""
+        bns = self._bns()
+        for i, bn in enumerate(bns):
+            if bn.running_mean is not self._blist[2 * i] or bn.running_var is not self._blist[2 * i + 1] \
+                    or bn.num_batches_tracked is not self._nlist[i]:
+                return False
         base = self._flat.data_ptr()
         o = 0
-        for p in self.parameters():
+        for p in self._plist:
             if p.data_ptr() != base + 4 * o or not p.is_contiguous():
                 return False
             o += p.numel()
         b = self._bn_flat.data_ptr()
         o = 0
-        for bn in self._bns():
-            for t in (bn.running_mean, bn.running_var):
-                if t.data_ptr() != b + 4 * o:
-                    return False
-                o += t.numel()
+        for t in self._blist:
+            if t.data_ptr() != b + 4 * o:
+                return False
+            o += t.numel()
         n = self._nbt_flat.data_ptr()
-        for i, bn in enumerate(self._bns()):
-            if bn.num_batches_tracked is not None and bn.num_batches_tracked.data_ptr() != n + 8 * i:
+        for i, t in enumerate(self._nlist):
+            if t is not None and t.data_ptr() != n + 8 * i:
                 return False
         return True
 
@@ -148,9 +160,11 @@ class EEGNet(nn.Module):
         bn = self.temporal[1]
         if bn.momentum is None:
             raise NotImplementedError("BatchNorm momentum=None (cumulative average) is not supported")
-        return Shape(C=self.C, T=self.T, F1=self.F1, D=self.D, K1=self.K1,
-                     p=float(self.aggregation[3].p), eps=float(bn.eps),
-                     momentum=float(bn.momentum))
+        key = (float(self.aggregation[3].p), float(bn.eps), float(bn.momentum))
+        if self._shape_cache is None or self._shape_cache[0] != key:
+            self._shape_cache = (key, Shape(C=self.C, T=self.T, F1=self.F1, D=self.D, K1=self.K1,
+                                            p=key[0], eps=key[1], momentum=key[2]))
+        return self._shape_cache[1]
 
     # -- dropout control (test hook) ------------------------------------------------------------
     def set_dropout_masks(self, m2, m3):

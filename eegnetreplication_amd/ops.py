@@ -56,8 +56,14 @@ class Shape:
         return self.T1 // 8
 
     def dims(self, B: int, p: float | None = None) -> _lib.Dims:
-        return _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1,
-                         self.p if p is None else p, self.eps, self.momentum)
+        if p is None:                 # per-B cache (the struct is only read by the library)
+            cache = self.__dict__.setdefault("_dims_cache", {})
+            d = cache.get(B)
+            if d is None:
+                d = cache[B] = _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1, self.p, self.eps,
+                                         self.momentum)
+            return d
+        return _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1, p, self.eps, self.momentum)
 
     def param_shapes(self):
         """(name, shape) in nn.Module.named_parameters() order (model.py:22-84)."""

@@ -141,8 +141,8 @@ def test_dropout_generator_properties():
     assert not torch.equal(l1, l3)
     # the injected-mask path and the generator path share the same kernels: with p = 0 both are
     # the identity and must agree bit for bit
-    from eegnetreplication_amd.ops import Shape
-    s0 = Shape(**{**shape.__dict__, "p": 0.0})
+    import dataclasses
+    s0 = dataclasses.replace(shape, p=0.0)
     a = ops.forward_train(s0, flat, bn.clone(), x, ws, 11, 1)
     b = ops.forward_train(s0, flat, bn.clone(), x, ws, 12, 7)
     assert torch.equal(a, b)
