@@ -213,12 +213,14 @@ __host__ __device__ constexpr int rup4(int a) { return (a + 3) & ~3; }
 __host__ __device__ constexpr int imax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int row_stride(int K1, int T) {
     // rows of x / s / dy / e: [LP zeros | T samples | >= R zeros]; long enough for the last 4-output
-    // FIR window and the last 16-column MFMA tile; RS/4 odd so that column reads of 16 rows (MFMA
+    // FIR window, the last 16-column MFMA tile and the last lag-correlation B tile of pass E; RS/4 odd so that column reads of 16 rows (MFMA
     // operands) land in 16 different bank groups
     const int P = (K1 - 1) / 2, R = K1 - 1 - P, LP = (R + 3) & ~3, OFF = LP - P, OFFD = LP - R;
     const int NW = (OFF + K1 + 6) / 4, TQ = (T + 3) / 4, NT16 = (T + 15) / 16;
     const int NW8 = (imax(OFF, OFFD) + K1 + 10) / 4, NO = (T + 7) / 8;     // 8-output windows
-    const int rs = rup4(imax(imax(imax(4 * (TQ - 1) + 4 * NW, 8 * (NO - 1) + 4 * NW8), LP + 16 * NT16), LP + T + R));
+    const int NWT = (15 + K1 - 1) / 16 + 1;                               // pass E lag-correlation tiles
+    const int rs = rup4(imax(imax(imax(imax(4 * (TQ - 1) + 4 * NW, 8 * (NO - 1) + 4 * NW8), LP + 16 * NT16), LP + T + R),
+                             OFF + 16 * (NT16 + NWT - 1)));
     return ((rs / 4) & 1) ? rs : rs + 4;
 }
 __host__ __device__ constexpr int row_stride2(int T) { return rup4(LP2 + T / 4 + 8); }

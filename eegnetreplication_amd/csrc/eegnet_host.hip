@@ -127,7 +127,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);
     g->ldsD = std::max(g->nwD * pwD, g->nwD * g->nD);
     g->ldsE = std::max(rows1 + 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4) + 8 * g->F2 + 64 * KSMAX,
-                       NWB * 256);                                // after the loop: dws tiles
+                       NWB * 256 * (1 + (15 + g->K1 - 1) / 16 + 1));   // after the loop: dws, Cq tiles
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
     auto tail = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + std::max(tail_scratch_doubles(ncols), fin)); };

@@ -565,12 +565,18 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     }
     const int NO = EEG_NO(TT);
     float sdyl = 0.f, sdyvl = 0.f;                   // this lane's row (half-wave) sums of dy, dy v
-    // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] of this lane's row, accumulated
-    // from the FIR's own s window (VALU: the f32 MFMA shares the vector pipe and its row-block
-    // formulation would cost 1.5x the MACs)
-    float Q[K1];
+    // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] on the matrix cores (a separate pipe
+    // from the FIR's VALU work).  With t = 16a + u and s'[i] = s[i-P]:
+    //     Cq[u][w] = sum_a dy[16a+u] s'[16a+w]        (16 x 16 NWT, K = the 16-sample blocks a)
+    //     Q[k]     = sum_u Cq[u][u+k]                  (diagonal sums, once, after the trial loop)
+    // Cq is linear in the trial, so it accumulates over the workgroup's trials in the MFMA
+    // accumulators (1.5x the MACs of the direct sum, none of its VALU issue slots or registers).
+    constexpr int NWT = (15 + K1 - 1) / 16 + 1;
+    floatx4 cq[RPW][NWT];
 #pragma unroll
-    for (int k = 0; k < K1; ++k) Q[k] = 0.f;
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int j = 0; j < NWT; ++j) cq[r][j] = (floatx4){0.f, 0.f, 0.f, 0.f};
     // dws GEMM split: wave -> (c-tile ct, k-group range)
     const int wpc = NWB / NCT;
     const bool gemm_on = wave < wpc * NCT;
@@ -658,11 +664,6 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                         sdyl += d;
                         sdyvl = fmaf(d, v[i], sdyvl);
                     }
-                    // Q[k] += sum_i dy[t0+i] s[t0+i+k-P]
-#pragma unroll
-                    for (int k = 0; k < K1; ++k)
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) Q[k] = fmaf(dy[i], w[G_::OFF + i + k], Q[k]);
                     lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
                     lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
                 }
@@ -680,24 +681,84 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                     xg[j] = (gemm_on && kg < kg1 && c < C) ? v : (floatx4){0.f, 0.f, 0.f, 0.f};
                 }
             }
-            // e[P+s] = sum_m w1[K1-1-m] dypad[s+m]  (transposed FIR) -> overwrites this row of s
-            if (oh < F2) {
-                const float* dyr = Dys + oh * RS;
+            // this wave's rows of the lag correlation (its own dy and s rows: the fence above orders
+            // them), then the transposed FIR e[P+s] = sum_m w1[K1-1-m] dypad[s+m] -> overwrites this
+            // row of s.  Specialised shapes (one octet per lane, every row live) run both as one
+            // straight-line block, the lag-correlation MFMAs spread through the FIR^T's FMAs so the
+            // matrix pipe works beside the VALU.
+            constexpr bool ONEOC = FF && TT && (EEG_NO(TT) <= 32) && (FF == RPW * NWB);
+            if constexpr (ONEOC) {
+                constexpr int NT16C = (TT + 15) / 16, KQC = (NT16C + 3) / 4, NQ = RPW * KQC * NWT;
+                const int oc = fir_oct(lane);
+                float w[4 * G_::NW8];
+                lds_window<G_::NW8>(Dys + oh * RS + 8 * oc, w);
+                float e[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) e[i] = 0.f;
+#pragma unroll
+                for (int m = 0; m < K1; ++m) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) e[i] = fmaf(tl[K1 - 1 - m], w[G_::OFFD + i + m], e[i]);
+                    // lag-correlation MFMAs n in [m NQ / K1, (m+1) NQ / K1)
+#pragma unroll
+                    for (int n = (m * NQ) / K1; n < ((m + 1) * NQ) / K1; ++n) {
+                        const int r = n / (KQC * NWT), ks = (n / NWT) % KQC, j = n % NWT;
+                        const int o = RPW * wave + r, a = 4 * ks + lk;
+                        const bool on = a < NT16C;
+                        const int ac = on ? a : 0;
+                        float av = Dys[o * RS + LP + li + 16 * ac];
+                        float bv = Ss[o * RS + G_::OFF + li + 16 * (ac + j)];
+                        av = on ? av : 0.f;
+                        bv = on ? bv : 0.f;
+                        cq[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, cq[r][j], 0, 0, 0);
+                    }
+                }
                 float* erow = Ss + oh * RS + LP;
-                for (int oc = fir_oct(lane); oc < NO; oc += 32) {
-                    float w[4 * G_::NW8];
-                    lds_window<G_::NW8>(dyr + 8 * oc, w);
-                    float e[8];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) e[i] = 0.f;
+                for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
+                lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
+                lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+            } else {
+                const int KQ = (NT16 + 3) >> 2;
 #pragma unroll
-                    for (int m = 0; m < K1; ++m)
+                for (int r = 0; r < RPW; ++r) {
+                    const int o = RPW * wave + r;
+                    if (o < F2) {
+                        const float* dyr = Dys + o * RS + LP + li;
+                        const float* sr = Ss + o * RS + G_::OFF + li;
+                        for (int ks = 0; ks < KQ; ++ks) {
+                            const int a = 4 * ks + lk;
+                            const bool on = a < NT16;
+                            const int ac = on ? a : 0;
+                            float av = dyr[16 * ac];
+                            av = on ? av : 0.f;
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) e[i] = fmaf(tl[K1 - 1 - m], w[G_::OFFD + i + m], e[i]);
+                            for (int j = 0; j < NWT; ++j) {
+                                float bv = sr[16 * (ac + j)];
+                                bv = on ? bv : 0.f;
+                                cq[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, cq[r][j], 0, 0, 0);
+                            }
+                        }
+                    }
+                }
+                if (oh < F2) {
+                    const float* dyr = Dys + oh * RS;
+                    float* erow = Ss + oh * RS + LP;
+                    for (int oc = fir_oct(lane); oc < NO; oc += 32) {
+                        float w[4 * G_::NW8];
+                        lds_window<G_::NW8>(dyr + 8 * oc, w);
+                        float e[8];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
-                    lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
-                    lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+                        for (int i = 0; i < 8; ++i) e[i] = 0.f;
+#pragma unroll
+                        for (int m = 0; m < K1; ++m)
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) e[i] = fmaf(tl[K1 - 1 - m], w[G_::OFFD + i + m], e[i]);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
+                        lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
+                        lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+                    }
                 }
             }
         }
@@ -775,13 +836,11 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     // ---- reductions ----
     float* row = part + (size_t)blockIdx.x * g.nE;
     {
-        // per-row sums: [Q K1][sdy][sdyv][pad 2]; a row's lanes (fir_row) are first gathered into
+        // per-row sums: [sdy][sdyv][pad 2]; a row's lanes (fir_row) are first gathered into
         // one half-wave (lane L of half h takes the lane that held octet L & 31 of row h)
-        constexpr int NR = K1 + 4, NH = NR / 2;
+        constexpr int NR = 4, NH = NR / 2;
         float rv[NR];
-#pragma unroll
-        for (int k = 0; k < K1; ++k) rv[k] = Q[k];
-        rv[K1] = sdyl; rv[K1 + 1] = sdyvl; rv[K1 + 2] = 0.f; rv[K1 + 3] = 0.f;
+        rv[0] = sdyl; rv[1] = sdyvl; rv[2] = 0.f; rv[3] = 0.f;
         {
             const int ocl = lane & 31;
             const int src = (ocl & 7) | ((ocl >> 3) << 4) | ((lane >> 5) << 3);
@@ -795,10 +854,31 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
 #pragma unroll
                 for (int j = 0; j < NH; ++j) {
                     const int idx = j + off;
-                    if (idx < K1) pub(row + (o * K1 + idx), rv[j]);
-                    else if (idx == K1) pub(row + (F2 * K1 + F2 * C + o), rv[j]);
-                    else if (idx == K1 + 1) pub(row + (F2 * K1 + F2 * C + F2 + o), rv[j]);
+                    if (idx == 0) pub(row + (F2 * K1 + F2 * C + o), rv[j]);
+                    else if (idx == 1) pub(row + (F2 * K1 + F2 * C + F2 + o), rv[j]);
                 }
+            }
+        }
+    }
+    // Q: this wave's Cq tiles -> its own LDS slice [16 u][16 NWT w] (past the dws tiles) -> diagonal sums
+    {
+        float* CQ = red + NWB * 256 + wave * (256 * NWT);
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int o = RPW * wave + r;
+            if (o < F2) {
+#pragma unroll
+                for (int j = 0; j < NWT; ++j)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) CQ[(4 * lk + q) * (16 * NWT) + 16 * j + li] = cq[r][j][q];
+                wave_lds_fence();
+                for (int k = lane; k < K1; k += 64) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) a += CQ[u * (16 * NWT) + u + k];
+                    pub(row + (o * K1 + k), a);
+                }
+                wave_lds_fence();
             }
         }
     }
