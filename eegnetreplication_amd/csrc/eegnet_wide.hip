@@ -966,7 +966,7 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
 // Wide pass E: dy2 and the weight-gradient reductions that need full-rate data, per o-chunk.
 // Partial row [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2] (other chunks' entries zero).
 // LDS: s rows, then e [16][RS] | dy rows [16][RS] | dp2 rows [16][T1] | coefficient table [16][8];
-// after the loop: dws tiles [NWW][256] and row sums
+// after the loop: dws tiles [NWW][256], row sums, lag-correlation tiles [NWW][16][16 NWT]
 // ================================================================================================
 template <int K1>
 __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const float* coef,
@@ -1004,9 +1004,13 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     }
     const int NO = (T + 7) >> 3;
     float sdyl = 0.f, sdyvl = 0.f;
-    float Qc[K1];
+    // this wave's row of the dW1 lag correlation on the matrix cores, as in k_pass_e:
+    // Cq[u][w] = sum_a dy[16a+u] s'[16a+w] accumulated over the trials, Q[k] = sum_u Cq[u][u+k]
+    constexpr int NWT = (15 + K1 - 1) / 16 + 1;
+    floatx4 cq[NWT];
 #pragma unroll
-    for (int k = 0; k < K1; ++k) Qc[k] = 0.f;
+    for (int jt = 0; jt < NWT; ++jt) cq[jt] = (floatx4){0.f, 0.f, 0.f, 0.f};
+    const int KQ = (NT16 + 3) >> 2;
     // dws GEMM split: wave -> (c-tile ct, k-group range)
     const int NCT = (C + 15) >> 4, wpc = NWW / NCT;
     const bool gemm_on = wave < wpc * NCT;
@@ -1046,15 +1050,28 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
                     sdyl += d;
                     sdyvl = fmaf(d, v[i], sdyvl);
                 }
-#pragma unroll
-                for (int k = 0; k < K1; ++k)
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) Qc[k] = fmaf(dy[i], w[G_::OFF + i + k], Qc[k]);
                 lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
                 lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
             }
         }
-        wave_lds_fence();                                  // dy row complete; s row consumed
+        wave_lds_fence();                                  // dy row complete
+        if (row_on) {                                      // lag correlation of this wave's row
+            const float* dyr = Dys + wave * RS + LP + li;
+            const float* sr = Ss + wave * RS + G_::OFF + li;
+            for (int ks = 0; ks < KQ; ++ks) {
+                const int a = 4 * ks + lk;
+                const bool on = a < NT16;
+                const int ac = on ? a : 0;
+                float av = dyr[16 * ac];
+                av = on ? av : 0.f;
+#pragma unroll
+                for (int jt = 0; jt < NWT; ++jt) {
+                    float bv = sr[16 * (ac + jt)];
+                    bv = on ? bv : 0.f;
+                    cq[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, cq[jt], 0, 0, 0);
+                }
+            }
+        }
         if (row_on) {                                      // e = FIR^T(dy) -> this wave's s row
             const float* dyr = Dys + wave * RS;
             float* erow = Ss + wave * RS + LP;
@@ -1102,25 +1119,20 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     }
 
     // ---- reductions ----
-    float* red = sm;                                       // [NWW][256] dws tiles | row sums
-    float* rsum = red + NWW * 256;                         // [16][K1 + 2]
+    float* red = sm;                                       // [NWW][256] dws tiles | row sums | Cq tiles
+    float* rsum = red + NWW * 256;                         // [16][2]: sdy, sdyv
+    float* CQ = rsum + 32;                                 // [NWW][16 u][16 NWT w]
 #pragma unroll
     for (int q = 0; q < 4; ++q) red[wave * 256 + (4 * lk + q) * 16 + li] = gemm_on ? xacc[q] : 0.f;
+#pragma unroll
+    for (int jt = 0; jt < NWT; ++jt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) CQ[wave * 256 * NWT + (4 * lk + q) * (16 * NWT) + 16 * jt + li] = cq[jt][q];
     {
-        constexpr int NR = (K1 + 2 + 3) / 4 * 4, NQ = NR / 4;    // [Q K1][sdy][sdyv][pad]
-        float rv[NR];
-#pragma unroll
-        for (int k = 0; k < K1; ++k) rv[k] = Qc[k];
-        rv[K1] = sdyl; rv[K1 + 1] = sdyvl;
-#pragma unroll
-        for (int i = K1 + 2; i < NR; ++i) rv[i] = 0.f;
-        wave_reduce<NR>(rv);
-        if ((lane & 15) == 0) {
-            const int r0 = (lane >> 4) * NQ;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q)
-                if (q + r0 < K1 + 2) rsum[wave * (K1 + 2) + q + r0] = rv[q];
-        }
+        float rv[4] = {sdyl, sdyvl, 0.f, 0.f};
+        wave_reduce<4>(rv);
+        if (lane == 0) rsum[2 * wave] = rv[0];
+        if (lane == 16) rsum[2 * wave + 1] = rv[0];
     }
     __syncthreads();
     float* row = part + (size_t)blockIdx.x * g.nE;
@@ -1129,7 +1141,11 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
         float v = 0.f;
         if (p < nQ) {                                       // Q[o][k]
             const int oq = p / K1, k = p - oq * K1, w = oq - o0;
-            if (w >= 0 && w < nrows) v = rsum[w * (K1 + 2) + k];
+            if (w >= 0 && w < nrows) {
+                const float* cw = CQ + w * 256 * NWT + k;
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v += cw[u * (16 * NWT + 1)];
+            }
         } else if (p < nQ + nX) {                           // Xm[o][c]
             const int pp = p - nQ, ox = pp / C, c = pp - ox * C, w = ox - o0;
             if (w >= 0 && w < nrows) {
@@ -1138,7 +1154,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
             }
         } else {                                            // Sdy, Sdyv
             const int pp = p - nQ - nX, os = pp < F2 ? pp : pp - F2, w = os - o0;
-            if (w >= 0 && w < nrows) v = rsum[w * (K1 + 2) + K1 + (pp < F2 ? 0 : 1)];
+            if (w >= 0 && w < nrows) v = rsum[2 * w + (pp < F2 ? 0 : 1)];
         }
         pub(row + p, v);
     }
