@@ -75,12 +75,14 @@ __device__ __forceinline__ void spatial_chunk(const float* __restrict__ xb, cons
         const int t = 16 * n + li;
         const bool ton = t < T;
         const int tc = ton ? t : T - 1;
+        // all KSW loads unconditional (clamped rows, lane-dependent masks only): a k-step guard
+        // (s < ks, wave-uniform) turns every load into a branch plus a full vmcnt wait
         float bv[KSW];
 #pragma unroll
         for (int s = 0; s < KSW; ++s) {
             const int c = 4 * s + lk;
             const float v = xb[(size_t)(c < C ? c : C - 1) * T + tc];
-            bv[s] = (s < ks && c < C && ton) ? v : 0.f;
+            bv[s] = (c < C && ton) ? v : 0.f;
         }
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
