@@ -176,7 +176,10 @@ static int make_geo_wide(Geo* g, bool launch) {
     const int nf4 = rup(g->NF, 4);
     auto tailw = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + fin); };
     const int awl = KSW * 64;                               // spatial GEMM fragment table
-    g->ldsWA = std::max((g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW + awl,
+    // after the loop pass A's Gram tiles [NWW][16][16 NWT] reuse the slice / s rows when they fit
+    const int cgw = NWW * 256 * ((15 + g->K1 - 1) / 16 + 1);
+    const int baseA = (g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW + awl;
+    g->ldsWA = std::max(baseA + ((g->CPC + 16) * g->RS >= cgw ? 0 : cgw),
                         tailw(g->nA, std::max(NTH, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C))));
     g->ldsWB = 16 * g->RS + awl;
     const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables

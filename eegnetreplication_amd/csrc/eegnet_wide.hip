@@ -157,9 +157,15 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
     for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + ((row_on ? o : 0) / g.D) * K1 + k];
     const int NO = (T + 7) >> 3;
     float svl = 0.f, sv2l = 0.f, s0 = 0.f;
-    float G0[K1];
+    // lag-Gram of this wave's slice channel on the matrix cores (the Hankel block product of pass E's
+    // lag correlation): with t' = 16a + u - P over the window [-P, T - P) of the zero-padded row,
+    // Cg[u][w] = sum_a xp[16a+u-P] xp[16a+w-P] accumulated over trials and G0[d] = sum_u Cg[u][u+d]
+    constexpr int NWT = (15 + K1 - 1) / 16 + 1;
+    floatx4 cg[NWT];
 #pragma unroll
-    for (int d = 0; d < K1; ++d) G0[d] = 0.f;
+    for (int jt = 0; jt < NWT; ++jt) cg[jt] = (floatx4){0.f, 0.f, 0.f, 0.f};
+    const int KQ = (NT16 + 3) >> 2;
+    const int li = lane & 15, lk = lane >> 4;
     float eacc[NEI];
     int ea[NEI], eb[NEI];
 #pragma unroll
@@ -190,20 +196,21 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
         spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
-        for (int q = tid; q < nc * TQ; q += NTW) {
-            const int c = q / TQ, qq = q - c * TQ;
-            float w[4 * G_::NW];
-            lds_window<G_::NW>(Xg + c * RS + 4 * qq, w);
-            float a[4];
+        for (int c = wave; c < nc; c += NWW) {
+            const float* xr = Xg + c * RS + G_::OFF + li;        // xp[i - P] = row[OFF + i]
+            for (int ks = 0; ks < KQ; ++ks) {
+                const int a = 4 * ks + lk;
+                const bool on = a < NT16;
+                const int ac = on ? a : 0;
+                float av = xr[16 * ac];
+                av = (on && 16 * ac + li < T) ? av : 0.f;        // window [-P, T - P)
+                s0 += av;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = (4 * qq + i < T) ? w[G_::OFF + i] : 0.f;
-            s0 += (a[0] + a[1]) + (a[2] + a[3]);
-#pragma unroll
-            for (int d = 0; d < K1; ++d) {
-                float acc = G0[d];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) acc = fmaf(a[i], w[G_::OFF + i + d], acc);
-                G0[d] = acc;
+                for (int jt = 0; jt < NWT; ++jt) {
+                    float bv = xr[16 * (ac + jt)];
+                    bv = on ? bv : 0.f;
+                    cg[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, cg[jt], 0, 0, 0);
+                }
             }
         }
 #pragma unroll
@@ -240,30 +247,34 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
     // ---- workgroup reduction -> one partial row (other chunks' Sv / Sv2 entries are zero) ----
     float* row = part + (size_t)blockIdx.x * g.nA;
     float* svw = red + NWW * (K1 + 1);               // [NWW][2]
+    // Gram tiles [NWW][16][16 NWT]: over the dead slice / s rows when they fit, else past the tables
+    // (eegnet_host.hip sizes ldsWA the same way)
+    float* CG = ((g.CPC + 16) * RS >= NWW * 256 * NWT) ? sm : awl + KSW * 64;
+    __syncthreads();
+#pragma unroll
+    for (int jt = 0; jt < NWT; ++jt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) CG[wave * 256 * NWT + (4 * lk + q) * (16 * NWT) + 16 * jt + li] = cg[jt][q];
     {
-        constexpr int NR = (K1 + 3 + 3) / 4 * 4, NQ = NR / 4;   // [G0 K1][s0][sv][sv2][pad]
-        float rv[NR];
-#pragma unroll
-        for (int d = 0; d < K1; ++d) rv[d] = G0[d];
-        rv[K1] = s0; rv[K1 + 1] = svl; rv[K1 + 2] = sv2l;
-#pragma unroll
-        for (int i = K1 + 3; i < NR; ++i) rv[i] = 0.f;
-        wave_reduce<NR>(rv);
-        if ((lane & 15) == 0) {
-            const int r0 = (lane >> 4) * NQ;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int idx = q + r0;
-                if (idx <= K1) red[wave * (K1 + 1) + idx] = rv[q];
-                else if (idx <= K1 + 2) svw[2 * wave + idx - K1 - 1] = rv[q];
-            }
-        }
+        float rv[4] = {s0, svl, sv2l, 0.f};                   // [s0][sv][sv2][pad]
+        wave_reduce<4>(rv);
+        if (lane == 0) red[wave * (K1 + 1) + K1] = rv[0];
+        if (lane == 16) svw[2 * wave] = rv[0];
+        if (lane == 32) svw[2 * wave + 1] = rv[0];
     }
     __syncthreads();
-    if (tid <= K1) {
+    if (tid < K1) {
         float t = 0.f;
-        for (int w = 0; w < NWW; ++w) t += red[w * (K1 + 1) + tid];
+        for (int w = 0; w < NWW; ++w) {
+            const float* cw = CG + w * 256 * NWT + tid;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t += cw[u * (16 * NWT + 1)];
+        }
         pub(row + tid, t);
+    } else if (tid == K1) {
+        float t = 0.f;
+        for (int w = 0; w < NWW; ++w) t += red[w * (K1 + 1) + K1];
+        pub(row + K1, t);
     }
 #pragma unroll
     for (int i = 0; i < NEI; ++i)
