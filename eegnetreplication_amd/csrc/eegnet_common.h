@@ -66,6 +66,7 @@ struct Geo {
     // F2 > 16 (eegnet_wide.hip): o-chunks of 16 rows, Gram electrode slice per chunk, block-2 rows
     // padded to F2P (32 / 64), block-2 row stride; LDS (floats) of the wide kernels
     int wide, NOC, CPC, F2P, RB, gridB2;
+    int splitC, splitD, splitE;   // wide passes whose reduction + finalize run in k_coltail (wide rows)
     int ldsWA, ldsWB, ldsWB2, ldsWC, ldsWD, ldsWE, ldsWI;
 };
 
@@ -148,7 +149,8 @@ enum PassCMode { PC_LOGITS = 1, PC_BWD = 2, PC_CE = 4 };
 // pass's finalize.  Ticket words: NCNT per pass, zeroed by a memset node at the start of every call.
 constexpr int KSMAX = 16;       // ws MFMA k-steps: ceil(C / 4), C <= 64
 constexpr int NGRPMAX = 32;      // groups <= NCNT - 1 (ticket words)
-constexpr int NCNT = 40;          // [0, ngrp) group tickets, [NCNT-1] the top-level ticket
+constexpr int NCNT = 40;
+constexpr int SPLIT_COLS = 2048;  // wide passes with more partial-row columns reduce in k_coltail          // [0, ngrp) group tickets, [NCNT-1] the top-level ticket
 constexpr int TK_PASSES = 5;      // ticket blocks: passes A..E, contiguous from pass A's
 struct FinArgs {
     double* part2;                // [ngrp][ncols] fp64 group partials

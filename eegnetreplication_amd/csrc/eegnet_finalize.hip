@@ -439,6 +439,46 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     if (tid == 0) *fa.step = s;
 }
 
+// ================================================================================================
+// Column-parallel tail for passes with wide partial rows (cfg5 EEGNet-16,4: passes C, D, E carry
+// 4-6 K columns per workgroup row).  The in-kernel two-level reduction funnels every column through
+// one workgroup at the top (ngrp x ncols doubles, ~1 MB at cfg5: tens of microseconds); here the pass
+// kernel only publishes its rows and NB = ceil(ncols / 64) workgroups each sum all rows of 64
+// columns in fp64 in a fixed row order (four row phases, combined in phase order), publish the
+// totals, and the last of them (ticket) stages the totals into LDS and runs the pass's finalize.
+// ================================================================================================
+constexpr int NTCT = 256;         // threads of k_coltail (64 columns x 4 row phases)
+template <int FIN>
+__global__ __launch_bounds__(NTCT) void k_coltail(Geo g, const float* prm, const float* part, int nrows, int ncols,
+                                                  FinArgs fa) {
+    extern __shared__ __attribute__((aligned(16))) double dsmt[];
+    const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    double* ph = dsmt + 2;                                 // [4][64] row-phase partials
+    double a = 0.0;
+    if (c < ncols) {
+        constexpr int NB8 = 8;                             // loads in flight per thread
+        for (int r0 = q; r0 < nrows; r0 += 4 * NB8) {
+            float v[NB8];
+#pragma unroll
+            for (int j = 0; j < NB8; ++j) v[j] = ld_pub(part + (size_t)min(r0 + 4 * j, nrows - 1) * ncols + c);
+#pragma unroll
+            for (int j = 0; j < NB8; ++j) a += r0 + 4 * j < nrows ? (double)v[j] : 0.0;
+        }
+    }
+    ph[q * 64 + lane] = a;
+    __syncthreads();
+    if (q == 0 && c < ncols) pub(fa.part2 + c, ((ph[lane] + ph[64 + lane]) + ph[128 + lane]) + ph[192 + lane]);
+    if (!take_ticket(fa.cnt + (NCNT - 1), gridDim.x, (int*)dsmt)) return;
+    double* S = dsmt + 2;
+    for (int i = tid; i < ncols; i += NTCT) S[i] = ld_pub(fa.part2 + i);
+    if (tid == 0) __hip_atomic_store(fa.cnt + (NCNT - 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if constexpr (FIN == 3) fin3(g, prm, S, fa);
+    else if constexpr (FIN == 4) fin4(g, prm, S, fa);
+    else fin5(g, prm, S, dsmt + tail_s_doubles(ncols), fa);
+}
+
 // torch.optim.Adam (weight_decay=0, amsgrad=False): torch/optim/adam.py:457,476,531-547
 __global__ __launch_bounds__(256) void k_adam(int64_t n, float* __restrict__ p, const float* __restrict__ gr,
                                              float* __restrict__ m, float* __restrict__ v,

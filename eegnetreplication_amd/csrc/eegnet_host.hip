@@ -173,6 +173,8 @@ static int make_geo_wide(Geo* g, bool launch) {
     if (G >= 8 * g->NOC) G = G / (8 * g->NOC) * (8 * g->NOC);
     g->gridS = G;
     g->grid = std::min(g->B, cus);                      // block-2 passes and the eval forward
+    // partial rows wider than this reduce in k_coltail (column-parallel) instead of in-kernel
+    g->splitC = g->nC > SPLIT_COLS; g->splitD = g->nD > SPLIT_COLS; g->splitE = g->nE > SPLIT_COLS;
     const int nf4 = rup(g->NF, 4);
     auto tailw = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + fin); };
     const int awl = KSW * 64;                               // spatial GEMM fragment table
@@ -239,11 +241,11 @@ static void set_key(Geo* g, uint64_t seed, uint64_t offset) {
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
 enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_INFER_BF16,
-                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_COUNT };
+                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_CTAIL, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
                                               "k_adam", "k_infer", "memset_tickets", "k_infer_bf16",
                                               "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c", "k_wpass_d",
-                                              "k_wpass_e", "k_winfer"};
+                                              "k_wpass_e", "k_winfer", "k_coltail"};
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { unsigned mask = 0; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
@@ -298,7 +300,8 @@ static void ensure_attrs() {
     set_attrs_wide<64>();
     for (const void* f : {(const void*)k_wpass_b2<NTB2>, (const void*)k_wpass_c<NTB2>, (const void*)k_wpass_d<NTB2>,
                           (const void*)k_wpass_c<256>, (const void*)k_wpass_d<256>,
-                          (const void*)k_wpass_c<256, true>, (const void*)k_wpass_d<256, true>})
+                          (const void*)k_wpass_c<256, true>, (const void*)k_wpass_d<256, true>,
+                          (const void*)k_coltail<3>, (const void*)k_coltail<4>, (const void*)k_coltail<5>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
                           (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>,
@@ -367,16 +370,31 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
         fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
     }
+    // the column-parallel reduction + finalize of a split pass (k_coltail, eegnet_finalize.hip)
+    auto coltail = [&](int fin, const float* part, int nrows, int ncols, const FinArgs& fa, int scr) {
+        const int nb = (ncols + 63) / 64;
+        const size_t lds = 8 * (size_t)std::max(2 + 4 * 64, tail_s_doubles(ncols) + scr);
+        PROF(KID_CTAIL);
+        if (fin == 3) hipLaunchKernelGGL(k_coltail<3>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
+        else if (fin == 4) hipLaunchKernelGGL(k_coltail<4>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
+        else hipLaunchKernelGGL(k_coltail<5>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
+    };
     { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
                                       (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
                                       (float*)(ws + L.partC), c_mode, fc, FoldCall{}); } LAUNCH_CHECK("k_wpass_c(bwd)");
+    if (g.splitC) { coltail(3, (const float*)(ws + L.partC), g.grid, g.nC, fc, 0); LAUNCH_CHECK("k_coltail(C)"); }
     { PROF(KID_WD); hipLaunchKernelGGL(k_wpass_d<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
                                       (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
                                       m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
     LAUNCH_CHECK("k_wpass_d");
+    if (g.splitD) { coltail(4, (const float*)(ws + L.partD), g.grid, g.nD, fd, 0); LAUNCH_CHECK("k_coltail(D)"); }
     { PROF(KID_WE); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
                                       (const float*)params, coef, x, (const float*)(ws + L.dp2),
                                       (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
+    if (g.splitE) {
+        coltail(5, (const float*)(ws + L.partE), g.gridS, g.nE, fe, fin5_scratch_doubles(g.K1, g.F1, g.o_g2));
+        LAUNCH_CHECK("k_coltail(E)");
+    }
     return 0;
 }
 

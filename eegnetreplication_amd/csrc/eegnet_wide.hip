@@ -750,6 +750,7 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
         pub(row + NCLS * NF + NCLS + 2 * F2, lossacc);
     }
     double* dsm = (double*)sm;
+    if (g.splitC) return;                            // k_coltail reduces and finalizes
     if (grid_reduce(g, part, g.nC, fa, dsm)) fin3(g, prm, dsm + 2, fa);
 }
 
@@ -972,6 +973,7 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
         pub(row + F2 * F2 + 16 * F2 + q, a);
     }
     double* dsm = (double*)sm;
+    if (g.splitD) return;                            // k_coltail reduces and finalizes
     if (grid_reduce(g, part, g.nD, fa, dsm)) fin4(g, prm, dsm + 2, fa);
 }
 
@@ -1172,6 +1174,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
         pub(row + p, v);
     }
     double* dsm = (double*)sm;
+    if (g.splitE) return;                            // k_coltail reduces and finalizes
     if (grid_reduce(g, part, g.nE, fa, dsm)) fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa);
 }
 

@@ -159,7 +159,7 @@ int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fo
 /* Optional per-kernel device timing for benchmarks: `on` is a bitmask of kernel ids (bit i = the
  * i-th name eegnet_profile_collect reports: k_pass_a, k_pass_b, k_pass_c, k_pass_d, k_pass_e,
  * k_adam, k_infer, memset_tickets, k_infer_bf16, k_wpass_a, k_wpass_b, k_wpass_b2, k_wpass_c,
- * k_wpass_d, k_wpass_e, k_winfer; -1 = all, 0 = off; the k_w* kernels are the F2 > 16 path).  Every selected kernel this
+ * k_wpass_d, k_wpass_e, k_winfer, k_coltail; -1 = all, 0 = off; the k_w* kernels are the F2 > 16 path).  Every selected kernel this
  * thread launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect
  * synchronises them and reports, per kernel name (32-byte slots in `names`), launch count and
  * summed device ms; it returns the number of kernels in *n_out.  Not for use under hipGraph
