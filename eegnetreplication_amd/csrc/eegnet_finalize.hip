@@ -447,28 +447,33 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
 // columns in fp64 in a fixed row order (four row phases, combined in phase order), publish the
 // totals, and the last of them (ticket) stages the totals into LDS and runs the pass's finalize.
 // ================================================================================================
-constexpr int NTCT = 256;         // threads of k_coltail (64 columns x 4 row phases)
+constexpr int NTCT = 1024;        // threads of k_coltail: 64 columns x 16 row phases
 template <int FIN>
 __global__ __launch_bounds__(NTCT) void k_coltail(Geo g, const float* prm, const float* part, int nrows, int ncols,
                                                   FinArgs fa) {
     extern __shared__ __attribute__((aligned(16))) double dsmt[];
+    constexpr int NPH = NTCT / 64, NB8 = 16;               // row phases; loads in flight per thread
     const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
     const int c = blockIdx.x * 64 + lane;
-    double* ph = dsmt + 2;                                 // [4][64] row-phase partials
+    double* ph = dsmt + 2;                                 // [NPH][64] row-phase partials
     double a = 0.0;
     if (c < ncols) {
-        constexpr int NB8 = 8;                             // loads in flight per thread
-        for (int r0 = q; r0 < nrows; r0 += 4 * NB8) {
+        for (int r0 = q; r0 < nrows; r0 += NPH * NB8) {
             float v[NB8];
 #pragma unroll
-            for (int j = 0; j < NB8; ++j) v[j] = ld_pub(part + (size_t)min(r0 + 4 * j, nrows - 1) * ncols + c);
+            for (int j = 0; j < NB8; ++j) v[j] = ld_pub(part + (size_t)min(r0 + NPH * j, nrows - 1) * ncols + c);
 #pragma unroll
-            for (int j = 0; j < NB8; ++j) a += r0 + 4 * j < nrows ? (double)v[j] : 0.0;
+            for (int j = 0; j < NB8; ++j) a += r0 + NPH * j < nrows ? (double)v[j] : 0.0;
         }
     }
     ph[q * 64 + lane] = a;
     __syncthreads();
-    if (q == 0 && c < ncols) pub(fa.part2 + c, ((ph[lane] + ph[64 + lane]) + ph[128 + lane]) + ph[192 + lane]);
+    if (q == 0 && c < ncols) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NPH; ++k) t += ph[k * 64 + lane];
+        pub(fa.part2 + c, t);
+    }
     if (!take_ticket(fa.cnt + (NCNT - 1), gridDim.x, (int*)dsmt)) return;
     double* S = dsmt + 2;
     for (int i = tid; i < ncols; i += NTCT) S[i] = ld_pub(fa.part2 + i);

@@ -373,7 +373,7 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
     // the column-parallel reduction + finalize of a split pass (k_coltail, eegnet_finalize.hip)
     auto coltail = [&](int fin, const float* part, int nrows, int ncols, const FinArgs& fa, int scr) {
         const int nb = (ncols + 63) / 64;
-        const size_t lds = 8 * (size_t)std::max(2 + 4 * 64, tail_s_doubles(ncols) + scr);
+        const size_t lds = 8 * (size_t)std::max(2 + (NTCT / 64) * 64, tail_s_doubles(ncols) + scr);
         PROF(KID_CTAIL);
         if (fin == 3) hipLaunchKernelGGL(k_coltail<3>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
         else if (fin == 4) hipLaunchKernelGGL(k_coltail<4>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
