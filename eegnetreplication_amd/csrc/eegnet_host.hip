@@ -26,7 +26,7 @@ static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
 constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 800 B, a multiple of 16
 
 struct WsLayout {
-    size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, total;
+    size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v, total;
 };
 
 static int device_cus() {
@@ -117,7 +117,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     const int rows1 = g->C * g->RS;                   // x rows (one buffer)
     const int nf4 = rup(g->NF, 4);
     g->ldsA = rows1 + g->F2 * g->RS + NWB * (g->K1 + 1);
-    g->ldsB = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + F2MAX * (K2 + F2MAX);
+    g->ldsB = 3 * g->F2 * g->RS2 + F2MAX * (K2 + F2MAX);
     // passes C / D: one trial stream per wave, each with its own block-2 rows (row_stride_b2)
     g->RSW = row_stride_b2(g->T1);
     const int pwC = nf4, pwD = 3 * g->F2 * g->RSW + nf4;
@@ -126,7 +126,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nwD = std::max(1, std::min(NTHS / 64, (LDS_MAX / 4) / pwD));
     g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);
     g->ldsD = std::max(g->nwD * pwD, g->nwD * g->nD);
-    g->ldsE = std::max(rows1 + 2 * g->F2 * g->RS + rup(g->F2 * g->T1, 4) + 8 * g->F2 + 64 * KSMAX,
+    g->ldsE = std::max((2 * g->F2 + g->C) * g->RS + rup(g->F2 * g->T1, 4) + 8 * g->F2,
                        NWB * 256 * (1 + (15 + g->K1 - 1) / 16 + 1));   // after the loop: dws, Cq tiles
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
@@ -220,6 +220,10 @@ static WsLayout make_layout(const Geo& g) {
     const size_t per = (size_t)g.B * g.F2 * g.T1 * 4;
     L.d2 = take(per); L.E1 = take(per); L.E2 = take(per); L.dp2 = take(per);
     L.dl = take((size_t)g.B * NCLS * 4);
+    // F2 <= 16: pass A's s [B][F2][T] and v [B][F2][8 ceil(T/8)] planes, read back by passes B and E
+    // (the wide path recomputes them)
+    L.s = take(g.wide ? 0 : (size_t)g.B * g.F2 * g.T * 4);
+    L.v = take(g.wide ? 0 : (size_t)g.B * g.F2 * ((g.T + 7) / 8 * 8) * 4);
     L.total = o;
     return L;
 }
@@ -407,17 +411,17 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
 #define LAUNCH_A(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsA * 4, s, \
-                                                   g, params, x, (float*)(ws + L.partA), fa, fc); \
+                                                   g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc); \
     else hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsA * 4, s, \
-                                                   g, params, x, (float*)(ws + L.partA), fa, fc)
+                                                   g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc)
     { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
     } LAUNCH_CHECK("k_pass_a");
 #define LAUNCH_B(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
-                       g, params, (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), \
-                       (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc); \
+                       g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
+                       (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc); \
     else hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
-                       g, params, (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2), (float*)(ws + L.E1), \
-                       (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc)
+                       g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
+                       (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc)
     { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
     } LAUNCH_CHECK("k_pass_b");
     return 0;
@@ -480,9 +484,11 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     } LAUNCH_CHECK("k_pass_d");
     }
 #define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
-                       g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc); \
+                       g, (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v), \
+                       (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc); \
     else hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
-                       g, (const float*)params, coef, x, (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc)
+                       g, (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v), \
+                       (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc)
     { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
     } LAUNCH_CHECK("k_pass_e");
     return 0;
@@ -768,7 +774,7 @@ int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fo
     fc.row0 = row0; fc.slot = slot; fc.koff = offset;
     fc.lr = lr; fc.b1 = beta1; fc.b2 = beta2; fc.eps = eps;
     fc.off = {L.cnt, L.partA, L.partB, L.partC, L.partD, L.partE, L.sums, L.stats, L.coef, L.d2, L.E1, L.E2,
-              L.dp2, L.dl};
+              L.dp2, L.dl, L.s, L.v};
     hipStream_t s = (hipStream_t)stream;
     FinArgs adam;                                     // non-null marker: pass E's finalize runs Adam
     memset(&adam, 0, sizeof(adam));

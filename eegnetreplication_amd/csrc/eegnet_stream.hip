@@ -47,6 +47,28 @@ __device__ __forceinline__ void x_dma(const float* __restrict__ xb, int C, int T
     }
 }
 
+// The same DMA issued from inline asm, so the compiler does not see an LDS write: its waitcnt pass
+// otherwise makes the next LDS read of ANY address wait (vmcnt) for the DMA to land, which turns a
+// prefetch issued ahead of a phase's LDS work into a stall at its first read.  The caller owns the
+// hand-off: the data is read only after a barrier preceded by a vmcnt wait that covers the DMA
+// (__syncthreads(), or barrier_vm<N> with N vector-memory operations issued after it).
+__device__ __forceinline__ void dma16(const float* gsrc, const float* ldst) {
+    const unsigned la = (unsigned)(size_t)(const __attribute__((address_space(3))) float*)ldst;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(gsrc), "s"(la) : "memory", "m0");
+}
+__device__ __forceinline__ void x_dma_asm(const float* __restrict__ xb, int C, int T, int RS, int LP, float* Xs,
+                                          int wave, int lane) {
+    const int np = T >> 8;
+    for (int i = wave; i < C * np; i += NWB) {
+        const int c = i / np, p = i - c * np;
+        dma16(xb + (size_t)c * T + 256 * p + 4 * lane, Xs + c * RS + LP + 256 * p);
+    }
+}
+__device__ __forceinline__ void flat_dma_asm(const float* __restrict__ src, int n, float* dst, int wave, int lane) {
+    for (int i = wave; i < (n >> 8); i += NWB) dma16(src + 256 * i + 4 * lane, dst + 256 * i);
+}
+
 // Zero the workgroup's LDS rows [0, n) before the first trial.  With LDS-DMA staging (SKIPX) the x
 // data windows [LP, LP + T) of the first C rows are left to the DMA, so fill and DMA touch disjoint
 // words and need no barrier between them (the barrier would also wait for every weight load).
@@ -69,6 +91,53 @@ __device__ __forceinline__ void zero_fill(float* sm, int n, int C, int RS, int L
 __device__ __forceinline__ void flat_dma(const float* __restrict__ src, int n, float* dst, int wave, int lane) {
     for (int i = wave; i < (n >> 8); i += NWB)
         __builtin_amdgcn_global_load_lds((gvoid_t*)(src + 256 * i + 4 * lane), (lvoid_t*)(dst + 256 * i), 16, 0, 0);
+}
+
+// workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not drain the wave's
+// global loads and stores (vmcnt); their register results are still waited for at first use
+__device__ __forceinline__ void barrier_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// the same after the wave's vector-memory operations except its N most recent have completed (vmcnt
+// counts loads, stores and LDS-DMA in issue order): LDS-DMA issued before those N has landed
+template <int N>
+__device__ __forceinline__ void barrier_vm() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(N) : "memory");
+}
+
+// one trial's s rows (LDS, [LP | T samples] per row) -> a contiguous [F2][T] block in global memory
+template <int NT>
+__device__ __forceinline__ void s_rows_store(const float* Ss, float* __restrict__ sb, int F2, int T, int RS, int LP,
+                                             int tid) {
+    if ((T & 3) == 0) {
+        const int TQ4 = T >> 2;
+        for (int i = tid; i < F2 * TQ4; i += NT) {
+            const int o = i / TQ4, q = i - o * TQ4;
+            *reinterpret_cast<floatx4*>(sb + 4 * i) = lds_ld4(Ss + o * RS + LP + 4 * q);
+        }
+    } else {
+        for (int i = tid; i < F2 * T; i += NT) {
+            const int o = i / T, t = i - o * T;
+            sb[i] = Ss[o * RS + LP + t];
+        }
+    }
+}
+
+// this wave's v octets (fir_row / fir_oct layout) of trial b from the v plane: MO octets of 8
+// samples per lane; unconditional loads at clamped addresses (a guarded load compiles to a branch
+// and a wait), so rows o >= F2 and octets >= NO hold copies that the callers never use
+template <int MO>
+__device__ __forceinline__ void v_load(const float* __restrict__ vg, int b, int F2, int NO, int oh, int lane,
+                                       float (&v)[MO][8]) {
+    const float* vrow = vg + ((size_t)b * F2 + min(oh, F2 - 1)) * (8 * NO);
+#pragma unroll
+    for (int m = 0; m < MO; ++m) {
+        const int oc = min(fir_oct(lane) + 32 * m, NO - 1);
+        const floatx4 a = *reinterpret_cast<const floatx4*>(vrow + 8 * oc);
+        const floatx4 c = *reinterpret_cast<const floatx4*>(vrow + 8 * oc + 4);
+        v[m][0] = a[0]; v[m][1] = a[1]; v[m][2] = a[2]; v[m][3] = a[3];
+        v[m][4] = c[0]; v[m][5] = c[1]; v[m][6] = c[2]; v[m][7] = c[3];
+    }
 }
 
 // this half-wave's taps (a per-lane select only when the two rows of a wave use different filters)
@@ -103,7 +172,8 @@ __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict_
 // ================================================================================================
 template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __restrict__ prm,
-                                                      const float* __restrict__ x, float* __restrict__ part,
+                                                      const float* __restrict__ x, float* __restrict__ sg,
+                                                      float* __restrict__ vg, float* __restrict__ part,
                                                       FinArgs fa, FoldCall fc) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
@@ -112,6 +182,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         const eegnet_fold& f = fc.folds[blockIdx.y];
         prm = f.params;
         x = f.x + fc.row0 * (long long)C * T;
+        sg = (float*)((char*)f.ws + fc.off.s);
+        vg = (float*)((char*)f.ws + fc.off.v);
         part = (float*)((char*)f.ws + fc.off.partA);
         fa = fold_fin(fc, f, TK_A, 1, 0, false, false, g.nparam);
     }
@@ -183,8 +255,6 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
-        if constexpr (!XDMA)
-            if (bn < b1) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
         spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
         // lag-Gram: items (c, quad), lanes of a wave on consecutive quads of one row
         for (int j = tid; j < C * TQ; j += NTB) {
@@ -226,25 +296,54 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
             }
         }
         TRACE_PH(g, 0, 0, tph_);
-        __syncthreads();                                   // Ss complete, x read for good
-        if constexpr (XDMA)
-            if (bn < b1) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+        barrier_lds();                                     // Ss complete, x read for good (LDS only:
+                                                           // the previous trial's v stores stay in flight)
+        if (bn < b1) {                                     // next x: lands by the closing barrier
+            if constexpr (XDMA) x_dma_asm(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+            else x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);   // live over the FIR only
+        }
         TRACE_PH(g, 0, 1, tph_);
-        // v = 32-tap FIR of this wave's s rows; BN2 sums of v
+        // s rows -> the s plane [B][F2][T] (pass E's lag-correlation operand)
+        s_rows_store<NTB>(Ss, sg + (size_t)b * F2 * T, F2, T, RS, LP, tid);
+        // v = 32-tap FIR of this wave's s rows; BN2 sums of v; v -> the v plane [B][F2][8 NO] (passes
+        // B and E read it back instead of recomputing the spatial GEMM and the FIR).  Compile-time
+        // shapes hold v in registers across the trial's closing barrier and store it after, so the
+        // barrier's vmcnt(0) -- there for the next x DMA -- does not wait for these stores.
+        const int hr = fir_row(lane), o = RPW * wave + hr;
+        float* const vrow = vg + ((size_t)b * F2 + (o < F2 ? o : 0)) * (8 * NO);
+        constexpr bool DEFER = XDMA;                       // (without DMA the barrier waits for no store)
+        constexpr int MOA = DEFER ? EEG_MO(TT) : 1;
+        float vs[MOA][8];
         {
-            const int hr = fir_row(lane), o = RPW * wave + hr;
             float tl[K1];
             half_taps<K1, NTS>(tap, hr, tl);
             if (o < F2) {
                 const float* row = Ss + o * RS;
-                for (int oc = fir_oct(lane); oc < NO; oc += 32) {
-                    float w[4 * G_::NW8];
-                    lds_window<G_::NW8>(row + 8 * oc, w);
-                    float v[8];
-                    fir8<K1, G_::OFF>(w, tl, v);
+                if constexpr (DEFER) {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
+                    for (int m = 0; m < MOA; ++m) {
+                        const int oc = fir_oct(lane) + 32 * m;
+                        if (oc < NO) {
+                            float w[4 * G_::NW8];
+                            lds_window<G_::NW8>(row + 8 * oc, w);
+                            fir8<K1, G_::OFF>(w, tl, vs[m]);
+#pragma unroll
+                            for (int i = 0; i < 8; ++i)
+                                if (8 * oc + i < T) { svl += vs[m][i]; sv2l = fmaf(vs[m][i], vs[m][i], sv2l); }
+                        }
+                    }
+                } else {
+                    for (int oc = fir_oct(lane); oc < NO; oc += 32) {
+                        float w[4 * G_::NW8];
+                        lds_window<G_::NW8>(row + 8 * oc, w);
+                        float v[8];
+                        fir8<K1, G_::OFF>(w, tl, v);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i)
+                            if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
+                        *reinterpret_cast<floatx4*>(vrow + 8 * oc) = (floatx4){v[0], v[1], v[2], v[3]};
+                        *reinterpret_cast<floatx4*>(vrow + 8 * oc + 4) = (floatx4){v[4], v[5], v[6], v[7]};
+                    }
                 }
             }
         }
@@ -252,7 +351,20 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         if constexpr (!XDMA)
             if (bn < b1) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         TRACE_PH(g, 0, 3, tph_);
-        __syncthreads();                                   // Xb staged, Ss free
+        if constexpr (XDMA) barrier_vm<0>();               // next x landed (asm DMA: explicit vmcnt), Ss free
+        else __syncthreads();                              // Xb staged, Ss free
+        if constexpr (DEFER) {
+            if (o < F2) {
+#pragma unroll
+                for (int m = 0; m < MOA; ++m) {
+                    const int oc = fir_oct(lane) + 32 * m;
+                    if (oc < NO) {
+                        *reinterpret_cast<floatx4*>(vrow + 8 * oc) = (floatx4){vs[m][0], vs[m][1], vs[m][2], vs[m][3]};
+                        *reinterpret_cast<floatx4*>(vrow + 8 * oc + 4) = (floatx4){vs[m][4], vs[m][5], vs[m][6], vs[m][7]};
+                    }
+                }
+            }
+        }
         TRACE_PH(g, 0, 4, tph_);
     }
     TRACE_LOOP(g, 0);
@@ -301,19 +413,20 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
 }
 
 // ================================================================================================
-// Pass B: forward to d2, E1/E2 (pooled ELU' sums for the BN2 backward), BN3 statistics.
+// Pass B: forward to d2, E1/E2 (pooled ELU' sums for the BN2 backward), BN3 statistics.  v comes
+// from pass A's v plane (no spatial GEMM, no FIR here): the pass streams 16 KB of v per trial in and
+// 12 KB of d2 / E1 / E2 out, with one workgroup barrier per trial.
 // part row: [Sr F2][Sr2 F2]
-// LDS: x rows | s rows | d2 rows (pad LP2) | q rows | weight table [w2 F2MAX x 16][W3 F2MAX x F2MAX]
+// LDS: d2 rows (pad LP2) | q rows x 2 (alternate trials) | weight table [w2 F2MAX x 16][W3 F2MAX x F2MAX]
 // ================================================================================================
 template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __restrict__ prm,
                                                       const float* coef,    // the finalize writes it: no __restrict__
-                                                      const float* __restrict__ x,
+                                                      const float* __restrict__ vg,
                                                       const uint8_t* __restrict__ mask2,
                                                       float* __restrict__ d2g, float* __restrict__ E1g,
                                                       float* __restrict__ E2g, float* __restrict__ part,
                                                       FinArgs fa, FoldCall fc) {
-    using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 1, TR_ENTRY);
     unsigned dk0;
@@ -322,7 +435,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
-        x = f.x + fc.row0 * (long long)C * T;
+        vg = (const float*)(ws + fc.off.v);
         mask2 = nullptr;
         d2g = (float*)(ws + fc.off.d2); E1g = (float*)(ws + fc.off.E1); E2g = (float*)(ws + fc.off.E2);
         part = (float*)(ws + fc.off.partB);
@@ -331,20 +444,16 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     } else {
         dk0 = drop_key(g, 0);
     }
-    constexpr int NTS = FF ? 1 : RPW;
-    const int D = FF ? 2 : g.D;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* const Xb = sm;              // one x buffer: the next trial lands after its last reader
-    float* Ss = sm + C * RS;
-    float* D2s = Ss + F2 * RS;
-    float* Qs = D2s + F2 * RS2;
-    float* Wt = Qs + F2 * RS2;         // block-2 weights, read with wave-uniform addresses
+    float* D2s = sm;
+    float* Qs0 = D2s + F2 * RS2;
+    float* Wt = Qs0 + 2 * F2 * RS2;    // block-2 weights, read with wave-uniform addresses
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int b0, b1;
     trial_range(g, b0, b1);
 
-    zero_fill<TT && (TT % 256 == 0)>(sm, (C + F2) * RS + 2 * F2 * RS2, C, RS, LP, T, tid);
+    for (int i = tid; i < 3 * F2 * RS2; i += NTB) sm[i] = 0.f;     // pads stay zero
     for (int i = tid; i < F2MAX * (K2 + F2MAX); i += NTB) {
         float v = 0.f;
         if (i < F2MAX * K2) { if (i < F2 * K2) v = prm[g.o_w2 + i]; }
@@ -354,86 +463,71 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         }
         Wt[i] = v;
     }
-    float aw[KS];
-    load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
-    float tap[NTS][K1];
-    load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
     const int NO = EEG_NO(TT);
+    constexpr int MO = EEG_MO(TT);
     float sr[RPW], sr2[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) { sr[r] = 0.f; sr2[r] = 0.f; }
     // BN2 constants of this lane's FIR row (fir_row)
+    const int hr = fir_row(lane), oh = RPW * wave + hr;
     float alh, beh, gah, bth;
     {
-        const int o = RPW * wave + fir_row(lane), oo = o < F2 ? o : 0;
+        const int oo = oh < F2 ? oh : 0;
         alh = coef[CF_AL2 * CSTR + oo]; beh = coef[CF_BE2 * CSTR + oo];
         gah = prm[g.o_g2 + oo]; bth = prm[g.o_b2 + oo];
     }
-    constexpr bool XDMA = TT && (TT % 256 == 0);
-    float pf[XDMA ? 1 : PF];
-    if constexpr (XDMA) {
-        if (b0 < b1) x_dma(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
-        __syncthreads();
-    } else {
-        if (b0 < b1) x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pf, tid);
-        __syncthreads();
-        x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
-        __syncthreads();
-    }
+    // v of the next trial rides one trial ahead in registers (compile-time shapes)
+    constexpr bool VPF = TT != 0;
+    float vpf[MO][8];
+    if (VPF && b0 < b1) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
+    __syncthreads();
 
     TRACE(g, 1, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
-        if constexpr (!XDMA)
-            if (bn < b1) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
-        spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+        float* Qs = Qs0 + ((b - b0) & 1) * F2 * RS2;
+        float vc[MO][8];
+        if constexpr (VPF) {
+#pragma unroll
+            for (int m = 0; m < MO; ++m)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) vc[m][i] = vpf[m][i];
+            if (bn < b1) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
+        } else {
+            v_load<MO>(vg, b, F2, NO, oh, lane, vc);
+        }
         TRACE_PH(g, 1, 0, tph_);
-        __syncthreads();                                   // Ss complete; Qs free; x read for good
-        if constexpr (XDMA)
-            if (bn < b1) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
-        TRACE_PH(g, 1, 1, tph_);
-        // d2 / E1 / E2 stay in registers until the next trial's x is staged: a global store issued
-        // before that x_store would hold its vmcnt wait (loads and stores drain in order)
-        constexpr int MO = EEG_MO(TT);
+        // BN2, ELU, pool4, dropout (model.py:47-50) of this lane's octets
         float d2v[MO][2], e1v[MO][2], e2v[MO][2];
-        const int hr = fir_row(lane), oh = RPW * wave + hr;
-        {
-            float tl[K1];
-            half_taps<K1, NTS>(tap, hr, tl);
-            if (oh < F2) {
-                const float* row = Ss + oh * RS;
-                float* drow = D2s + oh * RS2 + LP2;
+        if (oh < F2) {
+            float* drow = D2s + oh * RS2 + LP2;
 #pragma unroll
-                for (int m = 0; m < MO; ++m) {
-                    const int oc = fir_oct(lane) + 32 * m;
-                    if (oc >= NO) break;
-                    float w[4 * G_::NW8];
-                    lds_window<G_::NW8>(row + 8 * oc, w);
-                    float v[8];
-                    fir8<K1, G_::OFF>(w, tl, v);
+            for (int m = 0; m < MO; ++m) {
+                const int oc = fir_oct(lane) + 32 * m;
+                if (oc >= NO) break;
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {                // the octet's two pool-4 windows
-                        const int q = 2 * oc + h;
-                        float pe = 0.f, e1 = 0.f, e2 = 0.f;
+                for (int h = 0; h < 2; ++h) {                // the octet's two pool-4 windows
+                    const int q = 2 * oc + h;
+                    float pe = 0.f, e1 = 0.f, e2 = 0.f;
 #pragma unroll
-                        for (int i = 4 * h; i < 4 * h + 4; ++i) {
-                            const float xh = fmaf(alh, v[i], beh);
-                            const float z = fmaf(gah, xh, bth);
-                            const float dz = elu_d(z);
-                            pe += z > 0.f ? z : dz - 1.f;          // ELU(z) = exp(z) - 1 below 0
-                            e1 += dz;
-                            e2 = fmaf(dz, xh, e2);
-                        }
-                        const float d2 = q < T1 ? pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)((b * F2 + oh) * T1 + q)) : 0.f;
-                        d2v[m][h] = d2; e1v[m][h] = e1; e2v[m][h] = e2;
-                        if (q < T1) drow[q] = d2;
+                    for (int i = 4 * h; i < 4 * h + 4; ++i) {
+                        const float xh = fmaf(alh, vc[m][i], beh);
+                        const float z = fmaf(gah, xh, bth);
+                        const float dz = elu_d(z);
+                        pe += z > 0.f ? z : dz - 1.f;          // ELU(z) = exp(z) - 1 below 0
+                        e1 += dz;
+                        e2 = fmaf(dz, xh, e2);
                     }
+                    const float d2 = q < T1 ? pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)((b * F2 + oh) * T1 + q)) : 0.f;
+                    d2v[m][h] = d2; e1v[m][h] = e1; e2v[m][h] = e2;
+                    if (q < T1) drow[q] = d2;
                 }
             }
         }
         wave_lds_fence();
+        TRACE_PH(g, 1, 1, tph_);
         // depthwise 1x16 'same' conv of this wave's rows (model.py:54-61): pad 7 | 8
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
@@ -450,8 +544,6 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
             }
         }
         TRACE_PH(g, 1, 2, tph_);
-        if constexpr (!XDMA)
-            if (bn < b1) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         if (oh < F2) {
 #pragma unroll
             for (int m = 0; m < MO; ++m) {
@@ -468,7 +560,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
             }
         }
         TRACE_PH(g, 1, 3, tph_);
-        __syncthreads();                                   // Qs complete, Xb staged
+        // Qs complete.  The other q buffer is written by the next trial only after every wave has
+        // passed the next trial's barrier, i.e. finished this trial's pointwise reads below.  An
+        // LDS-only barrier: the d2 / E1 / E2 stores and the next trial's v loads stay in flight.
+        barrier_lds();
         TRACE_PH(g, 1, 4, tph_);
         // pointwise F2 x F2 (model.py:62-69) for this wave's rows; BN3 sums
         for (int t = lane; t < T1; t += 64) {
@@ -505,14 +600,19 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 }
 
 // ================================================================================================
-// Pass E: dy2 and the weight-gradient reductions that need full-rate data.
+// Pass E: dy2 and the weight-gradient reductions that need full-rate data.  s and v come from pass
+// A's planes (no spatial GEMM, no forward FIR here); x is read once, as the dws GEMM's operand.
 // part row: [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2]
-// LDS: x rows | s rows, then e | dy rows | dp2 [F2][T1]; after the loop: dws tiles | lag tiles
+// LDS: s rows | dy rows, then e rows | x rows | dp2 [F2][T1] | BN2 constants; after the loop: dws
+// tiles | lag tiles
+// Per trial: x DMA (for this trial's dws GEMM) | dy2 from v -> dy rows | lag correlation (dy, s) and
+// FIR^T (dy -> e, in place) | barrier | next trial's s / dp2 DMA and v loads | dws GEMM (e, x) | barrier
 // ================================================================================================
 template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,   // Adam (finalize) writes it
                                                       const float* coef,    // the finalize writes it: no __restrict__
                                                       const float* __restrict__ x,
+                                                      const float* __restrict__ sg, const float* __restrict__ vg,
                                                       const float* __restrict__ dp2g,
                                                       float* __restrict__ part, FinArgs fa, FoldCall fc) {
     using G_ = KG<K1>;
@@ -524,6 +624,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
         x = f.x + fc.row0 * (long long)C * T;
+        sg = (const float*)(ws + fc.off.s);
+        vg = (const float*)(ws + fc.off.v);
         dp2g = (const float*)(ws + fc.off.dp2);
         part = (float*)(ws + fc.off.partE);
         fa = fold_fin(fc, f, TK_E, 0, 0, false, true, g.nparam);
@@ -531,31 +633,27 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     constexpr int NTS = FF ? 1 : RPW;
     const int D = FF ? 2 : g.D;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* const Xb = sm;
-    float* Ss = sm + C * RS;                     // s, then e
-    float* Dys = Ss + F2 * RS;                   // dy2 (same padded layout)
-    float* DP = Dys + F2 * RS;                   // dp2 [F2][T1]
+    float* const Ss = sm;                        // s rows
+    float* const Dys = Ss + F2 * RS;             // dy2 rows, then (in place) e = FIR^T(dy2)
+    float* const Xb = Dys + F2 * RS;             // x rows (the dws GEMM's operand)
+    float* const DP = Xb + C * RS;               // dp2 [F2][T1]
     float* red = sm;                             // NWB * 256 dws tiles, reused after the trial loop
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int b0, b1;
     trial_range(g, b0, b1);
     const int li = lane & 15, lk = lane >> 4;
+    constexpr bool XDMA = TT && (TT % 256 == 0);
+    static_assert(!XDMA || (CC && FF), "LDS-DMA staging is specialised to compile-time C and F2");
 
     TRACE_PS(g, 0);
-    zero_fill<TT && (TT % 256 == 0)>(sm, (C + 2 * F2) * RS, C, RS, LP, T, tid);
+    zero_fill<XDMA>(sm, (2 * F2 + C) * RS, F2, RS, LP, T, tid);    // XDMA: the s data windows are the DMA's
     TRACE_PS(g, 1);
     float tap[NTS][K1];
     load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
     TRACE_PS(g, 2);
-    // BN2 forward / backward constants per row, [F2][8] in LDS (read per trial: seven loop-invariant
-    // registers less at the FIR^T, where the GEMM's x operand is already in flight)
+    // BN2 forward / backward constants per row, [F2][8] in LDS
     float* CT = DP + ((F2 * T1 + 3) & ~3);
-    float* AWL = CT + 8 * F2;                    // ws MFMA fragments [KS][64]
-    for (int i = tid; i < 64 * KS; i += NTB) {
-        const int s_ = i >> 6, o = lane & 15, c = 4 * s_ + (lane >> 4);
-        AWL[i] = (o < F2 && c < C) ? prm[g.o_ws + o * C + c] : 0.f;
-    }
     if (tid < 8 * F2) {
         const int o = tid >> 3, f = tid & 7;
         const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
@@ -564,9 +662,15 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         CT[tid] = src[o];
     }
     const int NO = EEG_NO(TT);
+    constexpr int MO = EEG_MO(TT);
+    const int hr = fir_row(lane), oh = RPW * wave + hr;
+    // specialised shapes with one octet per lane and every row live: e overwrites the dy rows in place;
+    // otherwise e goes to the s rows
+    constexpr bool ONEOC = FF && TT && (EEG_NO(TT) <= 32) && (FF == RPW * NWB);
+    float* const Eb = ONEOC ? Dys : Ss;
     float sdyl = 0.f, sdyvl = 0.f;                   // this lane's row (half-wave) sums of dy, dy v
-    // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] on the matrix cores (a separate pipe
-    // from the FIR's VALU work).  With t = 16a + u and s'[i] = s[i-P]:
+    // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] on the matrix cores.  With t = 16a + u
+    // and s'[i] = s[i-P]:
     //     Cq[u][w] = sum_a dy[16a+u] s'[16a+w]        (16 x 16 NWT, K = the 16-sample blocks a)
     //     Q[k]     = sum_u Cq[u][u+k]                  (diagonal sums, once, after the trial loop)
     // Cq is linear in the trial, so it accumulates over the workgroup's trials in the MFMA
@@ -583,8 +687,39 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     const int ct = gemm_on ? wave / wpc : 0, part_ = gemm_on ? wave - ct * wpc : 0;
     const int kg0 = (NT16 * part_) / wpc, kg1 = gemm_on ? (NT16 * (part_ + 1)) / wpc : 0;
     floatx4 xacc = {0.f, 0.f, 0.f, 0.f};
-    constexpr bool XDMA = TT && (TT % 256 == 0);
-    float pf[XDMA ? 1 : PF];
+    // s / x rows without DMA (T % 256 != 0) are staged through registers
+    constexpr int PFS = (FF && TT) ? ((FF * TT + NTB - 1) / NTB + 3) / 4 * 4 : MAXPF * NTH / NTB;
+    float pfs[XDMA ? 1 : PFS];
+    // without DMA each wave stages its own s rows (RPW rows, MS samples per lane per row), so only
+    // the wave itself reads them before its next barrier (the lag correlation reads own rows)
+    constexpr int MS = TT ? (TT + 63) / 64 : 16;
+    float pws[XDMA ? 1 : RPW][XDMA ? 1 : MS];
+    auto s_rows_load = [&](int bb) {
+        if constexpr (!XDMA) {
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const float* src = sg + ((size_t)bb * F2 + min(RPW * wave + r, F2 - 1)) * T;
+#pragma unroll
+                for (int k = 0; k < MS; ++k) pws[r][k] = src[min(lane + 64 * k, T - 1)];
+            }
+        }
+    };
+    auto s_rows_put = [&]() {
+        if constexpr (!XDMA) {
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int o = RPW * wave + r;
+#pragma unroll
+                for (int k = 0; k < MS; ++k)
+                    if (o < F2 && lane + 64 * k < T) Ss[o * RS + LP + lane + 64 * k] = pws[r][k];
+            }
+        }
+    };
+    float pfx[XDMA ? 1 : PF];
+    // v of the next trial: registers, loaded after the FIR^T (DMA shapes; the others load it at the
+    // top of the trial, keeping registers for the register-staged x and s rows)
+    constexpr bool VPF = XDMA;
+    float vpf[MO][8];
     // dp2 rows of the next trial ride along (registers, one trial ahead): a synchronous load would
     // wait (vmcnt is in order) for every memory operation issued before it
     constexpr int NDP = (CC && TT) ? (FF * (TT / 4) + NTB - 1) / NTB : 8;   // F2 * T1 <= NDP * NTB
@@ -592,34 +727,29 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     float pdp[NDP];
     // specialised shapes: dp2 rows go straight to LDS by DMA (no registers, no exposed load)
     constexpr bool DPDMA = TT && (TT % 256 == 0) && FF && ((FF * (TT / 4)) % 256 == 0);
-    // with LDS-DMA staging the dws GEMM reads its x operand straight from global memory (L2-warm:
-    // the same trial's x was just DMA'd), so the x buffer is free right after the spatial GEMM and
-    // the next trial's DMA overlaps the whole FIR / FIR^T phase
-    constexpr int NKGW = XDMA ? (TT / 16 + NWB / ((CC + 15) / 16) - 1) / (NWB / ((CC + 15) / 16)) : 1;
-    floatx4 xg[NKGW];
-    if constexpr (XDMA) {
-        if (b0 < b1) {
-            x_dma(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
-            TRACE_PS(g, 3);
-            if constexpr (DPDMA) flat_dma(dp2g + (size_t)b0 * ndp, ndp, DP, wave, lane);
-            else {
+    if (b0 < b1) {
+        if constexpr (XDMA) x_dma(sg + (size_t)b0 * F2 * T, F2, T, RS, LP, Ss, wave, lane);
+        else s_rows_load(b0);
+        TRACE_PS(g, 3);
+        if constexpr (DPDMA) flat_dma(dp2g + (size_t)b0 * ndp, ndp, DP, wave, lane);
+        else {
 #pragma unroll
             for (int j = 0; j < NDP; ++j) pdp[j] = dp2g[(size_t)b0 * ndp + min(tid + NTB * j, ndp - 1)];
 #pragma unroll
             for (int j = 0; j < NDP; ++j)
                 if (tid + NTB * j < ndp) DP[tid + NTB * j] = pdp[j];
             for (int i = tid + NTB * NDP; i < ndp; i += NTB) DP[i] = dp2g[(size_t)b0 * ndp + i];
-            }
-            TRACE_PS(g, 4);
         }
-        __syncthreads();
-    } else {
+        if constexpr (VPF) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
+        TRACE_PS(g, 4);
+    }
+    __syncthreads();
+    if constexpr (!XDMA) {
         if (b0 < b1) {
-            x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pf, tid);
-            for (int i = tid; i < ndp; i += NTB) DP[i] = dp2g[(size_t)b0 * ndp + i];
+            s_rows_put();
+            x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pfx, tid);
+            x_store<PF, NTB>(pfx, C, T, RS, LP, Xb, tid);
         }
-        __syncthreads();
-        x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         __syncthreads();
     }
 
@@ -628,65 +758,59 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
-        spatial_mfma_l<KS, NWB>(Xb, AWL, Ss, C, F2, NT16, RS, LP, wave, lane);
+        float vc[MO][8];
+        if constexpr (VPF) {
+#pragma unroll
+            for (int m = 0; m < MO; ++m)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) vc[m][i] = vpf[m][i];
+        } else {
+            v_load<MO>(vg, b, F2, NO, oh, lane, vc);
+        }
         TRACE_PH(g, 4, 0, tph_);
-        __syncthreads();                                   // Ss, DP complete
-        if constexpr (XDMA)
-            if (bn < b1) x_dma(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
+        // dy2 = A dz2 + B + C xh2 (BN2 backward) of this lane's octets; sums of dy and dy v
+        if (oh < F2) {
+            float* drow = Dys + oh * RS + LP;
+            const floatx4 c0 = lds_ld4(CT + 8 * oh), c1 = lds_ld4(CT + 8 * oh + 4);
+            const float alh = c0[0], beh = c0[1], gah = c0[2], bth = c0[3];
+            const float Aoh = c1[0], Boh = c1[1], Coh = c1[2];
+#pragma unroll
+            for (int m = 0; m < MO; ++m) {
+                const int oc = fir_oct(lane) + 32 * m;
+                if (oc >= NO) break;
+                float dpq[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) dpq[h] = (2 * oc + h < T1) ? DP[oh * T1 + 2 * oc + h] * 0.25f : 0.f;
+                float dy[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const bool in = 8 * oc + i < T;
+                    const float v = in ? vc[m][i] : 0.f;
+                    const float xh = fmaf(alh, v, beh);
+                    const float z = fmaf(gah, xh, bth);
+                    const float dz = dpq[i >> 2] * elu_d(z);
+                    float d = fmaf(Aoh, dz, fmaf(Coh, xh, Boh));
+                    d = in ? d : 0.f;
+                    dy[i] = d;
+                    sdyl += d;
+                    sdyvl = fmaf(d, v, sdyvl);
+                }
+                lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
+                lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
+            }
+        }
+        wave_lds_fence();                                  // dy rows complete
+        // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
+        // GEMM); they land during the lag correlation / FIR^T, by the next __syncthreads()
+        if constexpr (XDMA) x_dma_asm(x + (size_t)b * C * T, C, T, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 1, tph_);
         {
-            const int hr = fir_row(lane), oh = RPW * wave + hr;
             float tl[K1];
             half_taps<K1, NTS>(tap, hr, tl);
-            if (oh < F2) {
-                const float* row = Ss + oh * RS;
-                float* drow = Dys + oh * RS + LP;
-                const floatx4 c0 = lds_ld4(CT + 8 * oh), c1 = lds_ld4(CT + 8 * oh + 4);
-                const float alh = c0[0], beh = c0[1], gah = c0[2], bth = c0[3];
-                const float Aoh = c1[0], Boh = c1[1], Coh = c1[2];
-                for (int oc = fir_oct(lane); oc < NO; oc += 32) {
-                    float w[4 * G_::NW8];
-                    lds_window<G_::NW8>(row + 8 * oc, w);
-                    float v[8];
-                    fir8<K1, G_::OFF>(w, tl, v);
-                    float dpq[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) dpq[h] = (2 * oc + h < T1) ? DP[oh * T1 + 2 * oc + h] * 0.25f : 0.f;
-                    float dy[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const float xh = fmaf(alh, v[i], beh);
-                        const float z = fmaf(gah, xh, bth);
-                        const float dz = dpq[i >> 2] * elu_d(z);
-                        float d = fmaf(Aoh, dz, fmaf(Coh, xh, Boh));
-                        d = (8 * oc + i < T) ? d : 0.f;
-                        dy[i] = d;
-                        sdyl += d;
-                        sdyvl = fmaf(d, v[i], sdyvl);
-                    }
-                    lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
-                    lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
-                }
-            }
-            wave_lds_fence();                              // dy rows complete; s rows consumed
-            // this trial's x operand of the dws GEMM, issued here so the FIR^T covers its latency
-            // (the FIR^T holds fewer live registers than the forward FIR + lag correlation)
-            if constexpr (XDMA) {
-                const int c = ct * 16 + li;
-                const float* xr = x + ((size_t)b * C + (c < C ? c : 0)) * T + 4 * lk;
-#pragma unroll
-                for (int j = 0; j < NKGW; ++j) {
-                    const int kg = kg0 + j;
-                    const floatx4 v = *reinterpret_cast<const floatx4*>(xr + 16 * min(kg, NT16 - 1));
-                    xg[j] = (gemm_on && kg < kg1 && c < C) ? v : (floatx4){0.f, 0.f, 0.f, 0.f};
-                }
-            }
-            // this wave's rows of the lag correlation (its own dy and s rows: the fence above orders
-            // them), then the transposed FIR e[P+s] = sum_m w1[K1-1-m] dypad[s+m] -> overwrites this
-            // row of s.  Specialised shapes (one octet per lane, every row live) run both as one
-            // straight-line block, the lag-correlation MFMAs spread through the FIR^T's FMAs so the
-            // matrix pipe works beside the VALU.
-            constexpr bool ONEOC = FF && TT && (EEG_NO(TT) <= 32) && (FF == RPW * NWB);
+            // this wave's rows of the lag correlation (its own dy and s rows), then the transposed FIR
+            // e[P+s] = sum_m w1[K1-1-m] dypad[s+m], written over this wave's dy rows once every read
+            // of them is done.  Specialised shapes (one octet per lane, every row live) run both as one
+            // straight-line block, the lag-correlation MFMAs spread through the FIR^T's FMAs.
             if constexpr (ONEOC) {
                 constexpr int NT16C = (TT + 15) / 16, KQC = (NT16C + 3) / 4, NQ = RPW * KQC * NWT;
                 const int oc = fir_oct(lane);
@@ -713,9 +837,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                         cq[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, cq[r][j], 0, 0, 0);
                     }
                 }
-                float* erow = Ss + oh * RS + LP;
+                float* erow = Dys + oh * RS + LP;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
+                wave_lds_fence();                          // every dy read of this wave is done
                 lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
                 lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
             } else {
@@ -741,6 +866,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                         }
                     }
                 }
+                // e -> this wave's s rows (the lag correlation above was their last reader; a wave's
+                // LDS reads and writes stay in order)
                 if (oh < F2) {
                     const float* dyr = Dys + oh * RS;
                     float* erow = Ss + oh * RS + LP;
@@ -751,9 +878,9 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
 #pragma unroll
                         for (int i = 0; i < 8; ++i) e[i] = 0.f;
 #pragma unroll
-                        for (int m = 0; m < K1; ++m)
+                        for (int k = 0; k < K1; ++k)
 #pragma unroll
-                            for (int i = 0; i < 8; ++i) e[i] = fmaf(tl[K1 - 1 - m], w[G_::OFFD + i + m], e[i]);
+                            for (int i = 0; i < 8; ++i) e[i] = fmaf(tl[K1 - 1 - k], w[G_::OFFD + i + k], e[i]);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
                         lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
@@ -763,72 +890,66 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             }
         }
         TRACE_PH(g, 4, 2, tph_);
-        // the next trial's dp2 is fetched here (register staging only): its registers must not be
-        // live across the FIR / FIR^T phase (the kernel's register peak, 128 VGPRs at 4 waves/SIMD);
-        // the other workgroup on the CU covers the exposed latency
-        // (unconditional loads at clamped addresses: a guarded load compiles to a branch and a wait)
+        // the next trial's dp2 (register staging only; unconditional loads at clamped addresses)
         if (!DPDMA && bn < b1) {
 #pragma unroll
             for (int j = 0; j < NDP; ++j) pdp[j] = dp2g[(size_t)bn * ndp + min(tid + NTB * j, ndp - 1)];
         }
-        TRACE_PH(g, 4, 6, tph_);
-        __syncthreads();                                   // e rows complete
+        // e rows, x rows complete; s rows, dp2 consumed (the x DMA is asm: explicit vmcnt)
+        if constexpr (XDMA) barrier_vm<0>();
+        else __syncthreads();
         TRACE_PH(g, 4, 3, tph_);
-        if constexpr (DPDMA)                               // every DP reader is past: next trial's dp2
-            if (bn < b1) flat_dma(dp2g + (size_t)bn * ndp, ndp, DP, wave, lane);
+        if (bn < b1) {
+            if constexpr (XDMA) x_dma_asm(sg + (size_t)bn * F2 * T, F2, T, RS, LP, Ss, wave, lane);
+            else {                                         // registers over the dws GEMM only
+                s_rows_load(bn);
+                x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pfx, tid);
+            }
+            if constexpr (DPDMA) flat_dma_asm(dp2g + (size_t)bn * ndp, ndp, DP, wave, lane);
+            asm volatile("" ::: "memory");                 // the v loads issue after the DMA (barrier_vm)
+            if constexpr (VPF) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
+        }
         // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
         // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
         if (gemm_on) {
             const int c = ct * 16 + li;
-            const float* arow = Ss + (li < F2 ? li : 0) * RS + LP + 4 * lk;
+            const float* arow = Eb + (li < F2 ? li : 0) * RS + LP + 4 * lk;
+            const float* brow = Xb + (c < C ? c : 0) * RS + LP + 4 * lk;
             const bool aon = li < F2, bon = c < C;
-            if constexpr (XDMA) {
-#pragma unroll
-                for (int j = 0; j < NKGW; ++j) {
-                    const int kg = kg0 + j;
-                    if (kg < kg1) {
-                        floatx4 a4 = lds_ld4(arow + 16 * kg);
-                        if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                        const floatx4 b4 = xg[j];
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
-                    }
-                }
-            } else {
-                const float* brow = Xb + (c < C ? c : 0) * RS + LP + 4 * lk;
-                for (int kg = kg0; kg < kg1; ++kg) {
-                    floatx4 a4 = lds_ld4(arow + 16 * kg);
-                    floatx4 b4 = lds_ld4(brow + 16 * kg);
-                    if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                    if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
-                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
-                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
-                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
-                }
+            for (int kg = kg0; kg < kg1; ++kg) {
+                floatx4 a4 = lds_ld4(arow + 16 * kg);
+                floatx4 b4 = lds_ld4(brow + 16 * kg);
+                if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
             }
         }
-        if (!DPDMA && bn < b1) {                  // next trial's dp2 rows: every FIR reader is past
+        if (bn < b1) {
+            if constexpr (!DPDMA) {                        // next trial's dp2 rows: every reader is past
 #pragma unroll
-            for (int j = 0; j < NDP; ++j) {
-                const int i = tid + NTB * j;
-                if (i < ndp) DP[i] = pdp[j];
+                for (int j = 0; j < NDP; ++j) {
+                    const int i = tid + NTB * j;
+                    if (i < ndp) DP[i] = pdp[j];
+                }
             }
-            if constexpr (!XDMA) x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);
         }
         TRACE_PH(g, 4, 4, tph_);
-        __syncthreads();                                   // x and e rows consumed
-        TRACE_PH(g, 4, 5, tph_);
-        if constexpr (!XDMA) {
+        // (without DMA the next trial's x rows are stored right after the barrier: the next reader of
+        // the x buffer is that trial's dws GEMM, behind its first barrier)
+        // e, x rows consumed; next s rows and dp2 staged.  With both by DMA the barrier waits for the
+        // DMA only: the 2 MO v loads issued after it stay in flight into the next trial.
+        if constexpr (XDMA && DPDMA && VPF) barrier_vm<2 * MO>();
+        else if constexpr (XDMA || DPDMA) barrier_vm<0>();
+        else __syncthreads();
+        if constexpr (!XDMA)
             if (bn < b1) {
-                x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
-                TRACE_PH(g, 4, 6, tph_);
-                __syncthreads();                           // next trial's x staged
+                x_store<PF, NTB>(pfx, C, T, RS, LP, Xb, tid);
+                s_rows_put();
             }
-        }
-        TRACE_PH(g, 4, 7, tph_);
+        TRACE_PH(g, 4, 5, tph_);
     }
     TRACE_LOOP(g, 4);
     __syncthreads();

@@ -27,8 +27,8 @@ for line in out.splitlines():
 for k, v in rows.items():
     if filt not in k:
         continue
-    name = re.sub(r"_ZN3eeg\d+", "", k)[:18]
+    name = re.sub(r"_ZN3eeg\d+", "", k)[:34]
     g = lambda key: v.get(key, "?")
-    print(f"{name:18s} VGPR {g('VGPRs'):>4} AGPR {g('AGPRs'):>4} SGPR {g('TotalSGPRs'):>4} "
+    print(f"{name:34s} VGPR {g('VGPRs'):>4} AGPR {g('AGPRs'):>4} SGPR {g('TotalSGPRs'):>4} "
           f"vspill {g('VGPRs Spill'):>4} sspill {g('SGPRs Spill'):>3} scratch {g('ScratchSize [bytes/lane]'):>4} "
           f"occ {g('Occupancy [waves/SIMD]')}")
