@@ -217,7 +217,7 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
         }
         if (k == 0) {
             const double mu = m / n1;
-            const double var = q / n1 - mu * mu;
+            const double var = fmax(q / n1 - mu * mu, 0.0);   // E[u^2] - mu^2: never below 0
             const double inv = 1.0 / sqrt(var + (double)g.eps);
             const double a1 = (double)pg1[gg] * inv;
             const double c1 = (double)pb1[gg] - a1 * mu;
@@ -241,7 +241,7 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
         double W = 0.0;
         for (int c = 0; c < C; ++c) W += (double)pws[o * C + c];
         const double mv = Sv[o] / n2;
-        const double varv = Sv2[o] / n2 - mv * mv;
+        const double varv = fmax(Sv2[o] / n2 - mv * mv, 0.0);
         const double mu2 = a1s[gg] * mv + c1s[gg] * W;
         const double var2 = a1s[gg] * a1s[gg] * varv;
         const double inv2 = 1.0 / sqrt(var2 + (double)g.eps);
@@ -265,7 +265,7 @@ __device__ void fin2(const Geo& g, const double* sums, const FinArgs& fa) {
     if (j >= g.F2) return;
     const double n3 = (double)g.B * g.T1;
     const double mu = sums[j] / n3;
-    const double var = sums[g.F2 + j] / n3 - mu * mu;
+    const double var = fmax(sums[g.F2 + j] / n3 - mu * mu, 0.0);
     fa.coef[CF_MU3 * CSTR + j] = (float)mu;
     fa.coef[CF_INV3 * CSTR + j] = (float)(1.0 / sqrt(var + (double)g.eps));
     float* rm3 = fa.bn + 2 * g.F1 + 2 * g.F2;

@@ -57,6 +57,11 @@ __device__ __forceinline__ void dma16(const float* gsrc, const float* ldst) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(gsrc), "s"(la) : "memory", "m0");
 }
+__device__ __forceinline__ void dma4(const float* gsrc, const float* ldst) {    // 4 bytes per lane
+    const unsigned la = (unsigned)(size_t)(const __attribute__((address_space(3))) float*)ldst;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+                 :: "v"(gsrc), "s"(la) : "memory", "m0");
+}
 __device__ __forceinline__ void x_dma_asm(const float* __restrict__ xb, int C, int T, int RS, int LP, float* Xs,
                                           int wave, int lane) {
     const int np = T >> 8;
@@ -668,6 +673,12 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     // otherwise e goes to the s rows
     constexpr bool ONEOC = FF && TT && (EEG_NO(TT) <= 32) && (FF == RPW * NWB);
     float* const Eb = ONEOC ? Dys : Ss;
+    constexpr bool XDMA_ = TT && (TT % 256 == 0);
+    constexpr bool DPDMA_ = XDMA_ && FF && ((FF * (TT / 4)) % 256 == 0);
+    // the specialised pipeline (EEGNet-8,2 at T = 256): every wave DMAs its own rows of the next
+    // trial's dp2 (right after its dy2 phase) and s (right after its lag correlation), the next v is
+    // loaded a whole trial ahead, and the first barrier waits only for this trial's x
+    constexpr bool PIPEE = ONEOC && XDMA_ && DPDMA_ && (TT / 4 == 64) && (TT == 256);
     float sdyl = 0.f, sdyvl = 0.f;                   // this lane's row (half-wave) sums of dy, dy v
     // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] on the matrix cores.  With t = 16a + u
     // and s'[i] = s[i-P]:
@@ -764,6 +775,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             for (int m = 0; m < MO; ++m)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) vc[m][i] = vpf[m][i];
+            if constexpr (PIPEE)
+                if (bn < b1) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
         } else {
             v_load<MO>(vg, b, F2, NO, oh, lane, vc);
         }
@@ -799,11 +812,21 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
             }
         }
-        wave_lds_fence();                                  // dy rows complete
-        // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
-        // GEMM); they land during the lag correlation / FIR^T, by the next __syncthreads()
-        if constexpr (XDMA) x_dma_asm(x + (size_t)b * C * T, C, T, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 1, tph_);
+        wave_lds_fence();                                  // dy rows complete, this wave's dp2 rows read
+        if constexpr (PIPEE) {                             // next trial's dp2 rows of this wave
+            if (bn < b1) {
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    const int o = RPW * wave + r;
+                    dma4(dp2g + (size_t)bn * ndp + o * T1 + lane, DP + o * T1);
+                }
+            }
+        }
+        // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
+        // GEMM); they land during the lag correlation / FIR^T, by the next barrier
+        if constexpr (XDMA) x_dma_asm(x + (size_t)b * C * T, C, T, RS, LP, Xb, wave, lane);
+        TRACE_PH(g, 4, 2, tph_);
         {
             float tl[K1];
             half_taps<K1, NTS>(tap, hr, tl);
@@ -840,9 +863,18 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 float* erow = Dys + oh * RS + LP;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
-                wave_lds_fence();                          // every dy read of this wave is done
+                wave_lds_fence();                          // every dy / s read of this wave is done
                 lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
                 lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+                if constexpr (PIPEE) {                     // next trial's s rows of this wave
+                    if (bn < b1) {
+#pragma unroll
+                        for (int r = 0; r < RPW; ++r) {
+                            const int o = RPW * wave + r;
+                            dma16(sg + ((size_t)bn * F2 + o) * T + 4 * lane, Ss + o * RS + LP);
+                        }
+                    }
+                }
             } else {
                 const int KQ = (NT16 + 3) >> 2;
 #pragma unroll
@@ -889,17 +921,20 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 }
             }
         }
-        TRACE_PH(g, 4, 2, tph_);
+        TRACE_PH(g, 4, 3, tph_);
         // the next trial's dp2 (register staging only; unconditional loads at clamped addresses)
         if (!DPDMA && bn < b1) {
 #pragma unroll
             for (int j = 0; j < NDP; ++j) pdp[j] = dp2g[(size_t)bn * ndp + min(tid + NTB * j, ndp - 1)];
         }
         // e rows, x rows complete; s rows, dp2 consumed (the x DMA is asm: explicit vmcnt)
-        if constexpr (XDMA) barrier_vm<0>();
+        if constexpr (PIPEE) {                             // the RPW s DMAs of this wave may stay in flight
+            if (bn < b1) barrier_vm<RPW>();
+            else barrier_vm<0>();
+        } else if constexpr (XDMA) barrier_vm<0>();
         else __syncthreads();
-        TRACE_PH(g, 4, 3, tph_);
-        if (bn < b1) {
+        TRACE_PH(g, 4, 4, tph_);
+        if (!PIPEE && bn < b1) {
             if constexpr (XDMA) x_dma_asm(sg + (size_t)bn * F2 * T, F2, T, RS, LP, Ss, wave, lane);
             else {                                         // registers over the dws GEMM only
                 s_rows_load(bn);
@@ -909,6 +944,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             asm volatile("" ::: "memory");                 // the v loads issue after the DMA (barrier_vm)
             if constexpr (VPF) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
         }
+        TRACE_PH(g, 4, 5, tph_);
         // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
         // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
         if (gemm_on) {
@@ -936,12 +972,13 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 }
             }
         }
-        TRACE_PH(g, 4, 4, tph_);
+        TRACE_PH(g, 4, 6, tph_);
         // (without DMA the next trial's x rows are stored right after the barrier: the next reader of
         // the x buffer is that trial's dws GEMM, behind its first barrier)
         // e, x rows consumed; next s rows and dp2 staged.  With both by DMA the barrier waits for the
         // DMA only: the 2 MO v loads issued after it stay in flight into the next trial.
-        if constexpr (XDMA && DPDMA && VPF) barrier_vm<2 * MO>();
+        if constexpr (PIPEE) barrier_vm<0>();
+        else if constexpr (XDMA && DPDMA && VPF) barrier_vm<2 * MO>();
         else if constexpr (XDMA || DPDMA) barrier_vm<0>();
         else __syncthreads();
         if constexpr (!XDMA)
@@ -949,7 +986,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 x_store<PF, NTB>(pfx, C, T, RS, LP, Xb, tid);
                 s_rows_put();
             }
-        TRACE_PH(g, 4, 5, tph_);
+        TRACE_PH(g, 4, 7, tph_);
     }
     TRACE_LOOP(g, 4);
     __syncthreads();
