@@ -35,7 +35,9 @@ ALG_BYTES_PER_TRIAL = 45_056     # x read twice
 
 def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
     """Per-trial algorithmic FLOPs (MAC x 2) and HBM bytes of each pass kernel as implemented
-    (DESIGN.md section 4).  Returns {kernel: (flop, bytes)}."""
+    (DESIGN.md section 4).  Returns {kernel: (flop, bytes)}.  Pass A writes the s and v planes
+    ([F2, T] fp32 each) that pass B (v) and pass E (s, v) read instead of recomputing the spatial
+    GEMM and the FIR."""
     F2 = F1 * D
     T1, T2 = T // 4, T // 128
     npairs = K1 * (K1 - 1) // 2
@@ -44,12 +46,13 @@ def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
     b2 = F2 * T1 * 16 + F2 * F2 * T1  # block_2 forward (dw16 + pw)
     xb = C * T * 4
     row = F2 * T1 * 4
+    sv = F2 * ((T + 7) // 8 * 8) * 4  # one s / v plane row block of a trial
     return {
-        "k_pass_a": (2 * (sp + fir + C * T * K1 + 2 * C * npairs), xb),
-        "k_pass_b": (2 * (sp + fir + b2), xb + 3 * row),
+        "k_pass_a": (2 * (sp + fir + C * T * K1 + 2 * C * npairs), xb + 2 * sv),
+        "k_pass_b": (2 * b2, sv + 3 * row),
         "k_pass_c": (2 * (b2 + 2 * 4 * F2 * T2), row + 16),
         "k_pass_d": (2 * (b2 + 2 * F2 * F2 * T1 + 2 * F2 * T1 * 16), 4 * row + 16),
-        "k_pass_e": (2 * (sp + 3 * fir + sp), xb + row),
+        "k_pass_e": (2 * (2 * fir + sp), xb + 2 * sv + row),
     }
 
 
@@ -371,6 +374,7 @@ def main():
             roof = roofline_entry(dom, fl * B, by * B, dk[1] / dk[0] * 1e-3,
                                   pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc else None)
         impl_flop = sum(v[0] for v in alg.values())
+        impl_bytes = sum(v[1] for v in alg.values())
         infer = None
         if not args.no_infer:
             infer = bench_infer_bf16(dev, args.infer_batch, 64, 512, 16, 4, steps=20, warmup=3)
@@ -417,6 +421,9 @@ def main():
             "hbm_fraction": round(ALG_BYTES_PER_TRIAL * trials_per_s / (PEAK_HBM_GBS * 1e9), 4),
             "step_fp32_frac": round(impl_flop * trials_per_s / (PEAK_FP32_TFLOPS * 1e12), 4),
             "implemented_flop_per_trial": impl_flop,
+            # the step's own HBM traffic (x twice, the s / v planes, the block-2 planes) against peak
+            "implemented_bytes_per_trial": impl_bytes,
+            "step_hbm_frac": round(impl_bytes * trials_per_s / (PEAK_HBM_GBS * 1e9), 4),
             "x_buffers": args.nx,
             "ref_formulation_tflops": round(REF_FLOP_PER_TRIAL * trials_per_s / 1e12, 2),
             "kernels": per_kernel,
