@@ -183,7 +183,7 @@ static int make_geo_wide(Geo* g, bool launch) {
     const int baseA = (g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW + awl;
     g->ldsWA = std::max(baseA + ((g->CPC + 16) * g->RS >= cgw ? 0 : cgw),
                         tailw(g->nA, std::max(NTH, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C))));
-    g->ldsWB = 16 * g->RS + awl;
+    g->ldsWB = 0;                                           // k_wpass_b: registers only (v plane)
     const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables
     b2_lds(g, NWB2);
     g->gridB2 = g->grid;
@@ -220,10 +220,9 @@ static WsLayout make_layout(const Geo& g) {
     const size_t per = (size_t)g.B * g.F2 * g.T1 * 4;
     L.d2 = take(per); L.E1 = take(per); L.E2 = take(per); L.dp2 = take(per);
     L.dl = take((size_t)g.B * NCLS * 4);
-    // F2 <= 16: pass A's s [B][F2][T] and v [B][F2][8 ceil(T/8)] planes, read back by passes B and E
-    // (the wide path recomputes them)
-    L.s = take(g.wide ? 0 : (size_t)g.B * g.F2 * g.T * 4);
-    L.v = take(g.wide ? 0 : (size_t)g.B * g.F2 * ((g.T + 7) / 8 * 8) * 4);
+    // pass A's s [B][F2][T] and v [B][F2][8 ceil(T/8)] planes, read back by passes B and E
+    L.s = take((size_t)g.B * g.F2 * g.T * 4);
+    L.v = take((size_t)g.B * g.F2 * ((g.T + 7) / 8 * 8) * 4);
     L.total = o;
     return L;
 }
@@ -351,9 +350,10 @@ static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const flo
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
     { PROF(KID_WA); hipLaunchKernelGGL((k_wpass_a<K1>), dim3(g.gridS), dim3(NTW), g.ldsWA * 4, s, g, params, x,
-                                      (float*)(ws + L.partA), fa); } LAUNCH_CHECK("k_wpass_a");
+                                      (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa); }
+    LAUNCH_CHECK("k_wpass_a");
     { PROF(KID_WB); hipLaunchKernelGGL((k_wpass_b<K1>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g, params,
-                                      (const float*)(ws + L.coef), x, m2, (float*)(ws + L.d2),
+                                      (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2),
                                       (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
     { PROF(KID_WB2); hipLaunchKernelGGL(k_wpass_b2<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
                                       (const float*)(ws + L.d2), (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
@@ -393,8 +393,8 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
     LAUNCH_CHECK("k_wpass_d");
     if (g.splitD) { coltail(4, (const float*)(ws + L.partD), g.grid, g.nD, fd, 0); LAUNCH_CHECK("k_coltail(D)"); }
     { PROF(KID_WE); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
-                                      (const float*)params, coef, x, (const float*)(ws + L.dp2),
-                                      (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
+                                      (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v),
+                                      (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
     if (g.splitE) {
         coltail(5, (const float*)(ws + L.partE), g.gridS, g.nE, fe, fin5_scratch_doubles(g.K1, g.F1, g.o_g2));
         LAUNCH_CHECK("k_coltail(E)");

@@ -129,7 +129,8 @@ __device__ __forceinline__ void stage_slice(const float* __restrict__ xs, int nc
 // ================================================================================================
 template <int K1>
 __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict__ prm,
-                                                 const float* __restrict__ x, float* __restrict__ part,
+                                                 const float* __restrict__ x, float* __restrict__ sg,
+                                                 float* __restrict__ vg, float* __restrict__ part,
                                                  FinArgs fa) {
     using G_ = KG<K1>;
     constexpr int LP = G_::LP;
@@ -231,6 +232,9 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
         if (bn < b1 && nc > 0) stage_slice(x + ((size_t)bn * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
         if (row_on) {
             const float* row = Ss + wave * RS;
+            // this wave's s row -> the s plane [B][F2][T], its v octets -> the v plane [B][F2][8 NO]
+            // (passes B and E read them instead of recomputing the spatial GEMM and the FIR)
+            float* vrow = vg + ((size_t)b * F2 + o) * (8 * NO);
             for (int oc = lane; oc < NO; oc += 64) {
                 float w[4 * G_::NW8];
                 lds_window<G_::NW8>(row + 8 * oc, w);
@@ -239,6 +243,15 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                     if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
+                *reinterpret_cast<floatx4*>(vrow + 8 * oc) = (floatx4){v[0], v[1], v[2], v[3]};
+                *reinterpret_cast<floatx4*>(vrow + 8 * oc + 4) = (floatx4){v[4], v[5], v[6], v[7]};
+            }
+            float* srow = sg + ((size_t)b * F2 + o) * T;
+            if ((T & 3) == 0) {
+                for (int t = 4 * lane; t < T; t += 256)
+                    *reinterpret_cast<floatx4*>(srow + t) = lds_ld4(row + LP + t);
+            } else {
+                for (int t = lane; t < T; t += 64) srow[t] = row[LP + t];
             }
         }
         __syncthreads();                                   // next slice staged, s rows free
@@ -290,71 +303,81 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
 
 // ================================================================================================
 // Wide pass B: forward to the pooled block-2 input d2 = dropout(pool4(ELU(BN2(y2)))) and the pooled
-// ELU' sums E1 / E2 of the BN2 backward, per o-chunk.  No reduction (BN3's statistics are pass B2's).
+// ELU' sums E1 / E2 of the BN2 backward, per o-chunk.  v comes from pass A's v plane (one octet of
+// this wave's row per lane, the next trial's loaded a trial ahead): no LDS, no barrier.  No
+// reduction (BN3's statistics are pass B2's).
 // ================================================================================================
 template <int K1>
 __global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict__ prm, const float* coef,
-                                                 const float* __restrict__ x, const uint8_t* __restrict__ mask2,
+                                                 const float* __restrict__ vg, const uint8_t* __restrict__ mask2,
                                                  float* __restrict__ d2g, float* __restrict__ E1g,
                                                  float* __restrict__ E2g) {
-    using G_ = KG<K1>;
-    constexpr int LP = G_::LP;
-    const int C = g.C, T = g.T, F2 = g.F2, RS = g.RS, T1 = T >> 2, NT16 = (T + 15) >> 4;
+    const int T = g.T, F2 = g.F2, T1 = T >> 2;
     const unsigned dk0 = drop_key(g, 0);
-    extern __shared__ __attribute__((aligned(16))) float sm[];
     int j, b0, b1;
     wide_unit(g, j, b0, b1);
     const int o0 = 16 * j;
-    float* Ss = sm;
-    float* awl = Ss + 16 * RS;                         // ws fragments [KSW][64]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < 16 * RS; i += NTW) sm[i] = 0.f;
-    stage_aw_chunk(g, prm, o0, awl, tid, NTW);
+    (void)tid;
     const int o = o0 + wave;
     const bool row_on = o < F2;
     const int oo = row_on ? o : 0;
-    float tap[K1];
-#pragma unroll
-    for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + (oo / g.D) * K1 + k];
     const float alh = coef[CF_AL2 * CSTR + oo], beh = coef[CF_BE2 * CSTR + oo];
     const float gah = prm[g.o_g2 + oo], bth = prm[g.o_b2 + oo];
     const int NO = (T + 7) >> 3;
-    __syncthreads();
-    drain_prologue_loads();
+    constexpr int MOW = 4;                                 // octets per lane: T <= 2048
+    const int nmo = (NO + 63) >> 6;
+    auto vload = [&](int bb, float (&v)[MOW][8]) {
+        const float* vrow = vg + ((size_t)bb * F2 + oo) * (8 * NO);
+#pragma unroll
+        for (int m = 0; m < MOW; ++m) {
+            if (m < nmo) {
+                const int oc = min(lane + 64 * m, NO - 1);
+                const floatx4 a = *reinterpret_cast<const floatx4*>(vrow + 8 * oc);
+                const floatx4 c = *reinterpret_cast<const floatx4*>(vrow + 8 * oc + 4);
+                v[m][0] = a[0]; v[m][1] = a[1]; v[m][2] = a[2]; v[m][3] = a[3];
+                v[m][4] = c[0]; v[m][5] = c[1]; v[m][6] = c[2]; v[m][7] = c[3];
+            }
+        }
+    };
+    float vpf[MOW][8];
+    if (b0 < b1) vload(b0, vpf);
     for (int b = b0; b < b1; ++b) {
-        spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
-        __syncthreads();
+        float v[MOW][8];
+#pragma unroll
+        for (int m = 0; m < MOW; ++m)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[m][i] = vpf[m][i];
+        if (b + 1 < b1) vload(b + 1, vpf);
         if (row_on) {
-            const float* row = Ss + wave * RS;
             const size_t rb = ((size_t)b * F2 + o) * T1;
-            for (int oc = lane; oc < NO; oc += 64) {
-                float w[4 * G_::NW8];
-                lds_window<G_::NW8>(row + 8 * oc, w);
-                float v[8];
-                fir8<K1, G_::OFF>(w, tap, v);
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int q = 2 * oc + h;
-                    float pe = 0.f, e1 = 0.f, e2 = 0.f;
+            for (int m = 0; m < MOW; ++m) {
+                const int oc = lane + 64 * m;
+                if (m < nmo && oc < NO) {
 #pragma unroll
-                    for (int i = 4 * h; i < 4 * h + 4; ++i) {
-                        const float xh = fmaf(alh, v[i], beh);
-                        const float z = fmaf(gah, xh, bth);
-                        const float dz = elu_d(z);
-                        pe += z > 0.f ? z : dz - 1.f;
-                        e1 += dz;
-                        e2 = fmaf(dz, xh, e2);
-                    }
-                    if (q < T1) {
-                        d2g[rb + q] = pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q));
-                        E1g[rb + q] = e1;
-                        E2g[rb + q] = e2;
+                    for (int h = 0; h < 2; ++h) {
+                        const int q = 2 * oc + h;
+                        float pe = 0.f, e1 = 0.f, e2 = 0.f;
+#pragma unroll
+                        for (int i = 4 * h; i < 4 * h + 4; ++i) {
+                            const float xh = fmaf(alh, v[m][i], beh);
+                            const float z = fmaf(gah, xh, bth);
+                            const float dz = elu_d(z);
+                            pe += z > 0.f ? z : dz - 1.f;
+                            e1 += dz;
+                            e2 = fmaf(dz, xh, e2);
+                        }
+                        if (q < T1) {
+                            d2g[rb + q] = pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q));
+                            E1g[rb + q] = e1;
+                            E2g[rb + q] = e2;
+                        }
                     }
                 }
             }
         }
-        __syncthreads();                                   // s rows free
     }
 }
 
@@ -978,14 +1001,19 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
 }
 
 // ================================================================================================
-// Wide pass E: dy2 and the weight-gradient reductions that need full-rate data, per o-chunk.
+// Wide pass E: dy2 and the weight-gradient reductions that need full-rate data, per o-chunk.  s and v
+// come from pass A's planes; every wave stages and reads only its own s / dy / dp2 rows until the
+// dws GEMM, which reads all e rows of the chunk and x (global memory, L2).
 // Partial row [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2] (other chunks' entries zero).
-// LDS: s rows, then e [16][RS] | dy rows [16][RS] | dp2 rows [16][T1] | coefficient table [16][8];
-// after the loop: dws tiles [NWW][256], row sums, lag-correlation tiles [NWW][16][16 NWT]
+// LDS: s rows [16][RS] | dy rows, then (in place) e [16][RS] | dp2 rows [16][T1] | coefficient table
+// [16][8]; after the loop: dws tiles [NWW][256], row sums, lag-correlation tiles [NWW][16][16 NWT]
+// Per trial and wave: v (loaded a trial ahead) -> dy2 | next dp2 row (DMA) | lag correlation |
+// FIR^T -> e over the dy row | next s row (DMA) | barrier | dws GEMM | barrier
 // ================================================================================================
 template <int K1>
 __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const float* coef,
-                                                 const float* __restrict__ x, const float* __restrict__ dp2g,
+                                                 const float* __restrict__ x, const float* __restrict__ sg,
+                                                 const float* __restrict__ vg, const float* __restrict__ dp2g,
                                                  float* __restrict__ part, FinArgs fa) {
     using G_ = KG<K1>;
     constexpr int LP = G_::LP;
@@ -998,12 +1026,10 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     float* Dys = Ss + 16 * RS;
     float* DP = Dys + 16 * RS;
     float* CT = DP + ((16 * T1 + 3) & ~3);
-    float* awl = CT + 8 * 16;                          // ws fragments [KSW][64]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     for (int i = tid; i < 2 * 16 * RS; i += NTW) sm[i] = 0.f;
-    stage_aw_chunk(g, prm, o0, awl, tid, NTW);
     const int o = o0 + wave;
     const bool row_on = wave < nrows;
     const int oo = row_on ? o : 0;
@@ -1018,6 +1044,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
         CT[tid] = src[orr];
     }
     const int NO = (T + 7) >> 3;
+    constexpr int MOW = 2;                                 // octets per lane: T <= 1024
     float sdyl = 0.f, sdyvl = 0.f;
     // this wave's row of the dW1 lag correlation on the matrix cores, as in k_pass_e:
     // Cq[u][w] = sum_a dy[16a+u] s'[16a+w] accumulated over the trials, Q[k] = sum_u Cq[u][u+k]
@@ -1032,44 +1059,77 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     const int ct = gemm_on ? wave / wpc : 0, pt = gemm_on ? wave - ct * wpc : 0;
     const int kg0 = (NT16 * pt) / wpc, kg1 = gemm_on ? (NT16 * (pt + 1)) / wpc : 0;
     floatx4 xacc = {0.f, 0.f, 0.f, 0.f};
-    const int ndp = nrows * T1;
-    __syncthreads();
+    // this wave's s and dp2 rows of trial bb into LDS: LDS-DMA (inline asm: the caller's barrier_vm
+    // drains it) when the rows are whole 1 KiB / 256 B pieces, else synchronous copies
+    const bool rdma = (T & 255) == 0;
+    auto stage_rows = [&](int bb) {
+        if (!row_on) return;
+        const float* srow = sg + ((size_t)bb * F2 + o) * T;
+        const float* drow = dp2g + ((size_t)bb * F2 + o) * T1;
+        if (rdma) {
+            for (int p = 0; p < (T >> 8); ++p) dma16(srow + 256 * p + 4 * lane, Ss + wave * RS + LP + 256 * p);
+            for (int p = 0; p < (T1 >> 6); ++p) dma4(drow + 64 * p + lane, DP + wave * T1 + 64 * p);
+        } else {
+            for (int t = lane; t < T; t += 64) Ss[wave * RS + LP + t] = srow[t];
+            for (int t = lane; t < T1; t += 64) DP[wave * T1 + t] = drow[t];
+        }
+    };
+    auto vload = [&](int bb, float (&v)[MOW][8]) {
+        const float* vrow = vg + ((size_t)bb * F2 + oo) * (8 * NO);
+#pragma unroll
+        for (int m = 0; m < MOW; ++m) {
+            const int oc = min(lane + 64 * m, NO - 1);
+            const floatx4 a = *reinterpret_cast<const floatx4*>(vrow + 8 * oc);
+            const floatx4 c = *reinterpret_cast<const floatx4*>(vrow + 8 * oc + 4);
+            v[m][0] = a[0]; v[m][1] = a[1]; v[m][2] = a[2]; v[m][3] = a[3];
+            v[m][4] = c[0]; v[m][5] = c[1]; v[m][6] = c[2]; v[m][7] = c[3];
+        }
+    };
+    float vpf[MOW][8];
+    __syncthreads();                                       // zero fill before the first rows land
+    if (b0 < b1) { stage_rows(b0); vload(b0, vpf); }
+    barrier_vm<0>();
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
-        for (int i = tid; i < ndp; i += NTW) DP[i] = dp2g[((size_t)b * F2 + o0) * T1 + i];
-        spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
-        __syncthreads();                                   // s rows, dp2 rows complete
+        const int bn = b + 1;
+        float vc[MOW][8];
+#pragma unroll
+        for (int m = 0; m < MOW; ++m)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) vc[m][i] = vpf[m][i];
+        if (bn < b1) vload(bn, vpf);
         if (row_on) {
-            const float* row = Ss + wave * RS;
             float* drow = Dys + wave * RS + LP;
             const floatx4 c0v = lds_ld4(CT + 8 * wave), c1v = lds_ld4(CT + 8 * wave + 4);
             const float alh = c0v[0], beh = c0v[1], gah = c0v[2], bth = c0v[3];
             const float Aoh = c1v[0], Boh = c1v[1], Coh = c1v[2];
-            for (int oc = lane; oc < NO; oc += 64) {
-                float w[4 * G_::NW8];
-                lds_window<G_::NW8>(row + 8 * oc, w);
-                float v[8];
-                fir8<K1, G_::OFF>(w, tap, v);
-                float dpq[2];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) dpq[h] = (2 * oc + h < T1) ? DP[wave * T1 + 2 * oc + h] * 0.25f : 0.f;
-                float dy[8];
+            for (int m = 0; m < MOW; ++m) {
+                const int oc = lane + 64 * m;
+                if (oc < NO) {
+                    float dpq[2];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const float xh = fmaf(alh, v[i], beh);
-                    const float z = fmaf(gah, xh, bth);
-                    const float dz = dpq[i >> 2] * elu_d(z);
-                    float d = fmaf(Aoh, dz, fmaf(Coh, xh, Boh));
-                    d = (8 * oc + i < T) ? d : 0.f;
-                    dy[i] = d;
-                    sdyl += d;
-                    sdyvl = fmaf(d, v[i], sdyvl);
+                    for (int h = 0; h < 2; ++h) dpq[h] = (2 * oc + h < T1) ? DP[wave * T1 + 2 * oc + h] * 0.25f : 0.f;
+                    float dy[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const bool in = 8 * oc + i < T;
+                        const float v = in ? vc[m][i] : 0.f;
+                        const float xh = fmaf(alh, v, beh);
+                        const float z = fmaf(gah, xh, bth);
+                        const float dz = dpq[i >> 2] * elu_d(z);
+                        float d = fmaf(Aoh, dz, fmaf(Coh, xh, Boh));
+                        d = in ? d : 0.f;
+                        dy[i] = d;
+                        sdyl += d;
+                        sdyvl = fmaf(d, v, sdyvl);
+                    }
+                    lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
+                    lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
                 }
-                lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
-                lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
             }
         }
-        wave_lds_fence();                                  // dy row complete
+        wave_lds_fence();                                  // dy row complete, dp2 row read
         if (row_on) {                                      // lag correlation of this wave's row
             const float* dyr = Dys + wave * RS + LP + li;
             const float* sr = Ss + wave * RS + G_::OFF + li;
@@ -1087,31 +1147,43 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
                 }
             }
         }
-        if (row_on) {                                      // e = FIR^T(dy) -> this wave's s row
+        if (row_on) {                                      // e = FIR^T(dy) -> over this wave's dy row
             const float* dyr = Dys + wave * RS;
-            float* erow = Ss + wave * RS + LP;
-            for (int oc = lane; oc < NO; oc += 64) {
-                float w[4 * G_::NW8];
-                lds_window<G_::NW8>(dyr + 8 * oc, w);
-                float e[8];
+            float e[MOW][8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) e[i] = 0.f;
+            for (int m = 0; m < MOW; ++m) {
+                const int oc = lane + 64 * m;
+                if (oc < NO) {
+                    float w[4 * G_::NW8];
+                    lds_window<G_::NW8>(dyr + 8 * oc, w);
 #pragma unroll
-                for (int m = 0; m < K1; ++m)
+                    for (int i = 0; i < 8; ++i) e[m][i] = 0.f;
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) e[i] = fmaf(tap[K1 - 1 - m], w[G_::OFFD + i + m], e[i]);
+                    for (int k = 0; k < K1; ++k)
 #pragma unroll
-                for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
-                lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
-                lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+                        for (int i = 0; i < 8; ++i) e[m][i] = fmaf(tap[K1 - 1 - k], w[G_::OFFD + i + k], e[m][i]);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) e[m][i] = (8 * oc + i < T) ? e[m][i] : 0.f;
+                }
+            }
+            wave_lds_fence();                              // every dy / s read of this wave is done
+            float* erow = Dys + wave * RS + LP;
+#pragma unroll
+            for (int m = 0; m < MOW; ++m) {
+                const int oc = lane + 64 * m;
+                if (oc < NO) {
+                    lds_st4(erow + 8 * oc, (floatx4){e[m][0], e[m][1], e[m][2], e[m][3]});
+                    lds_st4(erow + 8 * oc + 4, (floatx4){e[m][4], e[m][5], e[m][6], e[m][7]});
+                }
             }
         }
-        __syncthreads();                                   // e rows complete
+        if (bn < b1) stage_rows(bn);                       // the next trial's s / dp2 rows of this wave
+        barrier_lds();                                     // e rows complete
         // Xm[o][c] += sum_t e[o][t] x[c][t]: A = e rows (LDS), B = x (global), float4 k-permuted
         if (gemm_on) {
             const int c = ct * 16 + li;
             const bool bon = c < C;
-            const float* arow = Ss + li * RS + LP + 4 * lk;
+            const float* arow = Dys + li * RS + LP + 4 * lk;
             const float* xr = x + ((size_t)b * C + (bon ? c : 0)) * T + 4 * lk;
             for (int kg = kg0; kg < kg1; ++kg) {
                 const int t0 = 16 * kg + 4 * lk;
@@ -1130,8 +1202,9 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
                 xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
             }
         }
-        __syncthreads();                                   // e rows and dp2 rows consumed
+        barrier_vm<0>();                                   // e rows consumed; next rows landed
     }
+    __syncthreads();
 
     // ---- reductions ----
     float* red = sm;                                       // [NWW][256] dws tiles | row sums | Cq tiles
