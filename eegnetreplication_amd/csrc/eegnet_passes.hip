@@ -487,6 +487,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             for (int n = 0; n < NCLS; ++n) dd = fmaf(dlv[n], wf[n][u], dd);
             if (i < NF) Hs[i] = dd * keep_mul(g, mask3, dk1, (unsigned)(b * NF + i));
         }
+        TRACE_PH(g, 3, 0, tph_);
         float q[F2MAX][MQ];
         dwconv_rows<MQ>(g, prm, F2, d, lane, q);
 #pragma unroll
@@ -497,6 +498,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                 if (o < F2 && t < T1) P1[o * RSW + LPQ + t] = q[o][m];
             }
         wave_lds_fence();
+        TRACE_PH(g, 3, 1, tph_);
         // BN3 backward with the batch constants of finalize 3: dr = A3 dz3 + B3 + C3 xh3,
         // dz3 = dp3/8 * ELU'(z3); zero beyond T1 (the dq / dd2 shifts read it)
         float dr[F2MAX][MQ];
@@ -524,6 +526,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             }
         }
         wave_lds_fence();
+        TRACE_PH(g, 3, 2, tph_);
         // E1 / E2 of pass B for the BN2-backward sums at the end (issued here, consumed last)
         float e1v[F2MAX][MQ], e2v[F2MAX][MQ];
         load_rows<MQ>(E1g, b, F2, T1, lane, e1v);
@@ -543,6 +546,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             }
         }
         wave_lds_fence();                          // q rows consumed before dq overwrites them
+        TRACE_PH(g, 3, 3, tph_);
         // dq[i][t] = sum_j W3[j][i] dr[j][t] (registers, and P1 for the dw2 correlation)
         float dq[F2MAX][MQ];
 #pragma unroll
@@ -566,6 +570,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             }
         }
         wave_lds_fence();
+        TRACE_PH(g, 3, 4, tph_);
         // dw2[o][k] += sum_t dq[o][t] d2p[o][t+k-7]: lane -> (row o2, taps 4 kq + kk), loop over t
         if (o2 < F2) {
             const float* dqr = P1 + o2 * RSW + LPQ;
@@ -580,6 +585,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                     for (int i = 0; i < 4; ++i) acc2[kk] = fmaf(a4[i], w[i + kk], acc2[kk]);
             }
         }
+        TRACE_PH(g, 3, 5, tph_);
         // dd2 = conv16_same_t(dq) -> dropout -> dp2; BN2-backward sums (E1/E2 of pass B)
         const size_t rb = (size_t)b * F2 * T1;
 #pragma unroll
@@ -601,6 +607,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             }
         }
         wave_lds_fence();
+        TRACE_PH(g, 3, 6, tph_);
     }
     TRACE_LOOP(g, 3);
     // ---- workgroup reduction ----
