@@ -124,9 +124,13 @@ def _run_units(specs, epochs, device, fold_batch):
     """Run unit specs one by one (_run_fold) or fold_batch at a time (_run_folds)."""
     if fold_batch <= 1:
         return [_run_fold(*sp[:5], sp[5], epochs, sp[6], device) for sp in specs]
+    # balanced batches of at most fold_batch units (90 cross-subject folds at 48: 45 + 45, not 48 + 42):
+    # one fold-indexed launch per pass serves a whole batch, so its size sets the launch width
+    nb = -(-len(specs) // fold_batch)
+    size = -(-len(specs) // nb) if nb else 0
     res = []
-    for i in range(0, len(specs), fold_batch):
-        res.extend(_run_folds(specs[i:i + fold_batch], epochs, device))
+    for i in range(0, len(specs), max(size, 1)):
+        res.extend(_run_folds(specs[i:i + size], epochs, device))
     return res
 
 
@@ -345,8 +349,9 @@ def main(argv=None) -> None:
     ap.add_argument("--generateReport", type=bool, default=True, help="Generate report after training.")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", type=str, default=".", help="directory for models/ and reports/")
-    ap.add_argument("--fold-batch", type=int, default=16,
-                    help="train this many folds together on one GPU (FoldBatch); 0/1: one at a time")
+    ap.add_argument("--fold-batch", type=int, default=48,
+                    help="train up to this many folds together on one GPU (FoldBatch, balanced batches); "
+                         "0/1: one at a time")
     ap.add_argument("--max-units", type=int, default=0,
                     help="smoke runs: only the first N folds of the protocol (0 = all)")
     ap.add_argument("--synthetic", action="store_true",

@@ -134,3 +134,25 @@ def test_device_loader_matches_dataloader_shuffle():
     plain = DataLoader(BCICI2ADataset(X, y), batch_size=64, shuffle=False)
     for (xa, ya), (xb, yb) in zip(DeviceLoader(X, y, 64, device="cpu"), plain):
         assert torch.equal(ya, yb) and torch.equal(xa, xb.float())
+
+
+def test_fold_batches_are_balanced(monkeypatch):
+    """_run_units splits the units into balanced fold batches of at most fold_batch (90 at 48: 45 + 45),
+    in unit order, and returns the results in unit order."""
+    from eegnetreplication_amd import train as T_
+    seen = []
+
+    def fake_run_folds(specs, epochs, device):
+        seen.append(len(specs))
+        return [sp for sp in specs]
+
+    monkeypatch.setattr(T_, "_run_folds", fake_run_folds)
+    specs = list(range(90))
+    assert T_._run_units(specs, 1, "cpu", 48) == specs
+    assert seen == [45, 45]
+    seen.clear()
+    assert T_._run_units(list(range(36)), 1, "cpu", 48) == list(range(36))
+    assert seen == [36]
+    seen.clear()
+    assert T_._run_units(list(range(10)), 1, "cpu", 4) == list(range(10))
+    assert seen == [4, 4, 2]
