@@ -600,7 +600,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                 if (t < T1) {
                     const int gi = o * T1 + t;
                     const float dp = a[m] * keep_mul(g, mask2, dk0, (unsigned)(rb + gi));
-                    dp2g[rb + gi] = dp;
+                    __builtin_nontemporal_store(dp, dp2g + rb + gi);
                     sz[o] = fmaf(dp * 0.25f, e1v[o][m], sz[o]);
                     sz[F2MAX + o] = fmaf(dp * 0.25f, e2v[o][m], sz[F2MAX + o]);
                 }

@@ -118,7 +118,7 @@ __device__ __forceinline__ void s_rows_store(const float* Ss, float* __restrict_
         const int TQ4 = T >> 2;
         for (int i = tid; i < F2 * TQ4; i += NT) {
             const int o = i / TQ4, q = i - o * TQ4;
-            *reinterpret_cast<floatx4*>(sb + 4 * i) = lds_ld4(Ss + o * RS + LP + 4 * q);
+            __builtin_nontemporal_store(lds_ld4(Ss + o * RS + LP + 4 * q), reinterpret_cast<floatx4*>(sb + 4 * i));
         }
     } else {
         for (int i = tid; i < F2 * T; i += NT) {
@@ -346,8 +346,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
 #pragma unroll
                         for (int i = 0; i < 8; ++i)
                             if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
-                        *reinterpret_cast<floatx4*>(vrow + 8 * oc) = (floatx4){v[0], v[1], v[2], v[3]};
-                        *reinterpret_cast<floatx4*>(vrow + 8 * oc + 4) = (floatx4){v[4], v[5], v[6], v[7]};
+                        __builtin_nontemporal_store((floatx4){v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
+                        __builtin_nontemporal_store((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
                     }
                 }
             }
@@ -364,8 +364,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
                 for (int m = 0; m < MOA; ++m) {
                     const int oc = fir_oct(lane) + 32 * m;
                     if (oc < NO) {
-                        *reinterpret_cast<floatx4*>(vrow + 8 * oc) = (floatx4){vs[m][0], vs[m][1], vs[m][2], vs[m][3]};
-                        *reinterpret_cast<floatx4*>(vrow + 8 * oc + 4) = (floatx4){vs[m][4], vs[m][5], vs[m][6], vs[m][7]};
+                        __builtin_nontemporal_store((floatx4){vs[m][0], vs[m][1], vs[m][2], vs[m][3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
+                        __builtin_nontemporal_store((floatx4){vs[m][4], vs[m][5], vs[m][6], vs[m][7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
                     }
                 }
             }
@@ -559,7 +559,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
                     const int q = 2 * oc + h;
                     if (q < T1) {
                         const size_t gi = ((size_t)b * F2 + oh) * T1 + q;
-                        d2g[gi] = d2v[m][h]; E1g[gi] = e1v[m][h]; E2g[gi] = e2v[m][h];
+                        __builtin_nontemporal_store(d2v[m][h], d2g + gi); __builtin_nontemporal_store(e1v[m][h], E1g + gi);
+                        __builtin_nontemporal_store(e2v[m][h], E2g + gi);
                     }
                 }
             }
