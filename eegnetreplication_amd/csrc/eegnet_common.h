@@ -540,32 +540,6 @@ __device__ __forceinline__ void spatial_mfma(const float* Xs, const float (&aw)[
     }
 }
 
-// the same with the ws fragments read from an LDS table [KS][64] (per tile: no registers held
-// across the caller's loop)
-template <int KS, int NW = NWAVE>
-__device__ __forceinline__ void spatial_mfma_l(const float* Xs, const float* awl, float* Ss, int C, int F2,
-                                               int NT16, int RS, int LP, int wave, int lane) {
-    const int li = lane & 15, lk = lane >> 4;
-    const int ks = (C + 3) >> 2;
-    for (int n = wave; n < NT16; n += NW) {
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        const float* xcol = Xs + lk * RS + LP + 16 * n + li;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            if (s < ks) {
-                const int c = 4 * s + lk;
-                const float b = (c < C) ? xcol[4 * s * RS] : 0.f;
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(awl[64 * s + lane], b, acc, 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int o = 4 * lk + r;
-            if (o < F2) Ss[o * RS + LP + 16 * n + li] = acc[r];
-        }
-    }
-}
-
 // Static shape of a kernel instantiation: CC/TT/FF = 0 means "runtime value from Geo".  The
 // specialised shapes are EEGNet-8,2 (F2 = 16, D = 2); PF = x prefetch floats per thread of an
 // NT_-thread workgroup.

@@ -699,10 +699,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     const int ct = gemm_on ? wave / wpc : 0, part_ = gemm_on ? wave - ct * wpc : 0;
     const int kg0 = (NT16 * part_) / wpc, kg1 = gemm_on ? (NT16 * (part_ + 1)) / wpc : 0;
     floatx4 xacc = {0.f, 0.f, 0.f, 0.f};
-    // s / x rows without DMA (T % 256 != 0) are staged through registers
-    constexpr int PFS = (FF && TT) ? ((FF * TT + NTB - 1) / NTB + 3) / 4 * 4 : MAXPF * NTH / NTB;
-    float pfs[XDMA ? 1 : PFS];
-    // without DMA each wave stages its own s rows (RPW rows, MS samples per lane per row), so only
+    // without DMA (T % 256 != 0) x rows are staged through registers (pfx, during the dws GEMM) and
+    // each wave stages its own s rows (RPW rows, MS samples per lane per row), so only
     // the wave itself reads them before its next barrier (the lag correlation reads own rows)
     constexpr int MS = TT ? (TT + 63) / 64 : 16;
     float pws[XDMA ? 1 : RPW][XDMA ? 1 : MS];
