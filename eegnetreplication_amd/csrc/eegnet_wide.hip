@@ -243,13 +243,13 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                     if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
-                *reinterpret_cast<floatx4*>(vrow + 8 * oc) = (floatx4){v[0], v[1], v[2], v[3]};
-                *reinterpret_cast<floatx4*>(vrow + 8 * oc + 4) = (floatx4){v[4], v[5], v[6], v[7]};
+                __builtin_nontemporal_store((floatx4){v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
+                __builtin_nontemporal_store((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
             }
             float* srow = sg + ((size_t)b * F2 + o) * T;
             if ((T & 3) == 0) {
                 for (int t = 4 * lane; t < T; t += 256)
-                    *reinterpret_cast<floatx4*>(srow + t) = lds_ld4(row + LP + t);
+                    __builtin_nontemporal_store(lds_ld4(row + LP + t), reinterpret_cast<floatx4*>(srow + t));
             } else {
                 for (int t = lane; t < T; t += 64) srow[t] = row[LP + t];
             }
@@ -370,9 +370,9 @@ __global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict_
                             e2 = fmaf(dz, xh, e2);
                         }
                         if (q < T1) {
-                            d2g[rb + q] = pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q));
-                            E1g[rb + q] = e1;
-                            E2g[rb + q] = e2;
+                            __builtin_nontemporal_store(pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q)), d2g + rb + q);
+                            __builtin_nontemporal_store(e1, E1g + rb + q);
+                            __builtin_nontemporal_store(e2, E2g + rb + q);
                         }
                     }
                 }
