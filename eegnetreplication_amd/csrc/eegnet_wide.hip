@@ -370,9 +370,9 @@ __global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict_
                             e2 = fmaf(dz, xh, e2);
                         }
                         if (q < T1) {
-                            __builtin_nontemporal_store(pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q)), d2g + rb + q);
-                            __builtin_nontemporal_store(e1, E1g + rb + q);
-                            __builtin_nontemporal_store(e2, E2g + rb + q);
+                            d2g[rb + q] = pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q));
+                            E1g[rb + q] = e1;
+                            E2g[rb + q] = e2;
                         }
                     }
                 }
