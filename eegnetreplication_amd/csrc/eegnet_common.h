@@ -177,7 +177,7 @@ enum { TK_A = 0, TK_B, TK_C, TK_D, TK_E, TK_COUNT };
 // Fold-indexed launches (eegnet_train_step_folds): blockIdx.y is the fold; a fold's pointers come
 // from its eegnet_fold entry and its workspace regions sit at the same offsets in every workspace.
 struct WsOff {
-    unsigned long long cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v;
+    unsigned long long cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v, q3, r3;
 };
 struct FoldCall {
     const eegnet_fold* folds;     // nullptr: single-model launch (pointers from the kernel arguments)

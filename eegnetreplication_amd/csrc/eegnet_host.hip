@@ -26,7 +26,7 @@ static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
 constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 800 B, a multiple of 16
 
 struct WsLayout {
-    size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v, total;
+    size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v, q3, r3, total;
 };
 
 static int device_cus() {
@@ -223,6 +223,10 @@ static WsLayout make_layout(const Geo& g) {
     // pass A's s [B][F2][T] and v [B][F2][8 ceil(T/8)] planes, read back by passes B and E
     L.s = take((size_t)g.B * g.F2 * g.T * 4);
     L.v = take((size_t)g.B * g.F2 * ((g.T + 7) / 8 * 8) * 4);
+    // F2 <= 16: pass B's block-2 depthwise output q and pointwise output r [B][F2][T/4], read by passes
+    // C (r) and D (q, r) instead of recomputing them from d2
+    L.q3 = take(g.wide ? 0 : per);
+    L.r3 = take(g.wide ? 0 : per);
     L.total = o;
     return L;
 }
@@ -418,10 +422,12 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
     } LAUNCH_CHECK("k_pass_a");
 #define LAUNCH_B(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
                        g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
-                       (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc); \
+                       (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
+                       (float*)(ws + L.partB), fb, fc); \
     else hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
                        g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
-                       (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.partB), fb, fc)
+                       (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
+                       (float*)(ws + L.partB), fb, fc)
     { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
     } LAUNCH_CHECK("k_pass_b");
     return 0;
@@ -446,10 +452,10 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
         fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
     }
 #define LAUNCH_CB(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF, true>), dim3(g.grid, nf), dim3(64 * g.nwC), g.ldsC * 4, s, \
-                       g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
+                       g, params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits, \
                        (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc); \
     else hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid, nf), dim3(64 * g.nwC), g.ldsC * 4, s, \
-                       g, params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits, \
+                       g, params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits, \
                        (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc)
     if (use_b2_narrow(g)) {
         { PROF(KID_C);
@@ -474,11 +480,13 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     } LAUNCH_CHECK("k_pass_c(bwd)");
 #define LAUNCH_D(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, true>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
-                       (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2), \
+                       (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
+                       m2, m3, dl, (float*)(ws + L.dp2), \
                        (float*)(ws + L.partD), fd, fc); \
     else hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
-                       (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2), \
+                       (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
+                       m2, m3, dl, (float*)(ws + L.dp2), \
                        (float*)(ws + L.partD), fd, fc)
     { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
     } LAUNCH_CHECK("k_pass_d");
@@ -613,7 +621,7 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
         return 0;
     }
 #define LAUNCH_CF(K, CC, TT, FF) hipLaunchKernelGGL((k_pass_c<K, CC, TT, FF>), dim3(g.grid), dim3(64 * g.nwC), g.ldsC * 4, s, \
-                       g, params, (const float*)(w + L.coef), (const float*)(w + L.d2), mask3, (const float*)nullptr, \
+                       g, params, (const float*)(w + L.coef), (const float*)(w + L.r3), mask3, (const float*)nullptr, \
                        (const int64_t*)nullptr, logits, (float*)nullptr, (float*)nullptr, (int)PC_LOGITS, none, \
                        FoldCall{})
     { PROF(KID_C);
@@ -774,7 +782,7 @@ int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fo
     fc.row0 = row0; fc.slot = slot; fc.koff = offset;
     fc.lr = lr; fc.b1 = beta1; fc.b2 = beta2; fc.eps = eps;
     fc.off = {L.cnt, L.partA, L.partB, L.partC, L.partD, L.partE, L.sums, L.stats, L.coef, L.d2, L.E1, L.E2,
-              L.dp2, L.dl, L.s, L.v};
+              L.dp2, L.dl, L.s, L.v, L.q3, L.r3};
     hipStream_t s = (hipStream_t)stream;
     FinArgs adam;                                     // non-null marker: pass E's finalize runs Adam
     memset(&adam, 0, sizeof(adam));

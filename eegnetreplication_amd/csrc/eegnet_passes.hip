@@ -86,31 +86,7 @@ __device__ __forceinline__ void shl1(float (&x)[MQ], int lane) {
     }
 }
 
-// y[t] = sum_k w[k] x[t + k - 7]: depthwise 1x16 'same' conv (model.py:54-61, pad 7 | 8); x is
-// zero outside [0, T1)
-template <int MQ>
-__device__ __forceinline__ void conv16_same(const float (&x)[MQ], const float* __restrict__ w, float (&y)[MQ],
-                                            int lane) {
-    float s[MQ];
-#pragma unroll
-    for (int m = 0; m < MQ; ++m) { y[m] = w[7] * x[m]; s[m] = x[m]; }
-#pragma unroll
-    for (int k = 6; k >= 0; --k) {                 // s = x[t - (7 - k)]
-        shr1<MQ>(s, lane);
-#pragma unroll
-        for (int m = 0; m < MQ; ++m) y[m] = fmaf(w[k], s[m], y[m]);
-    }
-#pragma unroll
-    for (int m = 0; m < MQ; ++m) s[m] = x[m];
-#pragma unroll
-    for (int k = 8; k < K2; ++k) {                 // s = x[t + k - 7]
-        shl1<MQ>(s, lane);
-#pragma unroll
-        for (int m = 0; m < MQ; ++m) y[m] = fmaf(w[k], s[m], y[m]);
-    }
-}
-
-// its transpose: y[t] = sum_k w[k] x[t + 7 - k] (the input gradient of conv16_same)
+// transposed depthwise 1x16: y[t] = sum_k w[k] x[t + 7 - k] (the input gradient of the 'same' conv, model.py:54-61)
 template <int MQ>
 __device__ __forceinline__ void conv16_same_t(const float (&x)[MQ], const float* __restrict__ w, float (&y)[MQ],
                                               int lane) {
@@ -148,44 +124,15 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ src, int b, 
         }
 }
 
-// q = conv16_same of every d2 row, each row's taps scalar-loaded next to their use
+// xh[j] = BN3-normalised r[j] (batch statistics of finalize 2), r from pass B's r plane
 template <int MQ>
-__device__ __forceinline__ void dwconv_rows(const Geo& g, const float* __restrict__ prm, int F2,
-                                            const float (&d)[F2MAX][MQ], int lane, float (&q)[F2MAX][MQ]) {
-#pragma unroll
-    for (int o = 0; o < F2MAX; ++o) {
-        if (o < F2) {
-            const int oz = o >= 2 ? opaque0_after(q[o >= 2 ? o - 2 : 0][0]) : opaque0();   // one row of lookahead
-            conv16_same<MQ>(d[o], prm + (g.o_w2 + o * K2 + oz), q[o], lane);
-        } else {
-#pragma unroll
-            for (int m = 0; m < MQ; ++m) q[o][m] = 0.f;
-        }
-    }
-}
-
-// xh[j] = BN3-normalised r[j] = sum_i W3[j][i] q[i] (model.py:62-71; batch statistics of finalize 2)
-template <int MQ>
-__device__ __forceinline__ void pw_bn3(const Geo& g, const float* __restrict__ prm, const float* coef, int F2,
-                                       const float (&q)[F2MAX][MQ], float (&xh)[F2MAX][MQ]) {
+__device__ __forceinline__ void bn3_rows(const float* coef, int F2, const float (&r)[F2MAX][MQ],
+                                         float (&xh)[F2MAX][MQ]) {
 #pragma unroll
     for (int j = 0; j < F2MAX; ++j) {
-        if (j < F2) {
-            const int oz = j >= 2 ? opaque0_after(xh[j >= 2 ? j - 2 : 0][0]) : opaque0();
-            const float* w3 = prm + (g.o_W3 + j * F2 + oz);
-            const float mu3 = coef[CF_MU3 * CSTR + j + oz], inv3 = coef[CF_INV3 * CSTR + j + oz];
+        const float mu3 = j < F2 ? coef[CF_MU3 * CSTR + j] : 0.f, inv3 = j < F2 ? coef[CF_INV3 * CSTR + j] : 0.f;
 #pragma unroll
-            for (int m = 0; m < MQ; ++m) {
-                float r = 0.f;
-#pragma unroll
-                for (int i = 0; i < F2MAX; ++i)
-                    if (i < F2) r = fmaf(w3[i], q[i][m], r);
-                xh[j][m] = (r - mu3) * inv3;
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < MQ; ++m) xh[j][m] = 0.f;
-        }
+        for (int m = 0; m < MQ; ++m) xh[j][m] = (r[j][m] - mu3) * inv3;
     }
 }
 
@@ -198,7 +145,7 @@ __device__ __forceinline__ void pw_bn3(const Geo& g, const float* __restrict__ p
 template <int K1, int CC, int TT, int FF, bool FOLD = false>
 __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* __restrict__ prm,
                                                 const float* coef,    // the finalize writes it: no __restrict__
-                                                const float* __restrict__ d2g,
+                                                const float* __restrict__ r3g,
                                                 const uint8_t* __restrict__ mask3,
                                                 const float* __restrict__ dlin,
                                                 const int64_t* __restrict__ labels,
@@ -212,7 +159,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
-        d2g = (const float*)(ws + fc.off.d2);
+        r3g = (const float*)(ws + fc.off.r3);
         mask3 = nullptr; dlin = nullptr; logits = nullptr;
         labels = f.labels + fc.row0;
         dlout = (float*)(ws + fc.off.dl);
@@ -252,12 +199,12 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     for (int b = blockIdx.x * nw + wave; b < g.B; b += gridDim.x * nw) {
         float xh[F2MAX][MQ];
         {
-            float d[F2MAX][MQ], q[F2MAX][MQ];
-            load_rows<MQ>(d2g, b, F2, T1, lane, d);
+            // block 2 up to the pointwise mix is pass B's (its r plane): BN3 normalisation only
+            float r[F2MAX][MQ];
+            load_rows<MQ>(r3g, b, F2, T1, lane, r);
             TRACE_PH(g, 2, 0, tph_);
-            dwconv_rows<MQ>(g, prm, F2, d, lane, q);
+            bn3_rows<MQ>(coef, F2, r, xh);
             TRACE_PH(g, 2, 1, tph_);
-            pw_bn3<MQ>(g, prm, coef, F2, q, xh);
         }
         // ELU -> AvgPool(1,8) -> Hs (flattened index j*T2 + t/8)
 #pragma unroll
@@ -403,6 +350,8 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                                                  const float* __restrict__ d2g,
                                                  const float* __restrict__ E1g,
                                                  const float* __restrict__ E2g,
+                                                 const float* __restrict__ q3g,
+                                                 const float* __restrict__ r3g,
                                                  const uint8_t* __restrict__ mask2,
                                                  const uint8_t* __restrict__ mask3,
                                                  const float* __restrict__ dl,
@@ -418,6 +367,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
         coef = (const float*)(ws + fc.off.coef);
         d2g = (const float*)(ws + fc.off.d2);
         E1g = (const float*)(ws + fc.off.E1); E2g = (const float*)(ws + fc.off.E2);
+        q3g = (const float*)(ws + fc.off.q3); r3g = (const float*)(ws + fc.off.r3);
         mask2 = nullptr; mask3 = nullptr;
         dl = (const float*)(ws + fc.off.dl);
         dp2g = (float*)(ws + fc.off.dp2);
@@ -488,8 +438,8 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             if (i < NF) Hs[i] = dd * keep_mul(g, mask3, dk1, (unsigned)(b * NF + i));
         }
         TRACE_PH(g, 3, 0, tph_);
-        float q[F2MAX][MQ];
-        dwconv_rows<MQ>(g, prm, F2, d, lane, q);
+        float q[F2MAX][MQ];                     // block-2 depthwise output: pass B's q plane
+        load_rows<MQ>(q3g, b, F2, T1, lane, q);
 #pragma unroll
         for (int o = 0; o < F2MAX; ++o)
 #pragma unroll
@@ -504,7 +454,11 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
         float dr[F2MAX][MQ];
         {
             float xh[F2MAX][MQ];
-            pw_bn3<MQ>(g, prm, coef, F2, q, xh);
+            {
+                float r[F2MAX][MQ];                 // pointwise output: pass B's r plane
+                load_rows<MQ>(r3g, b, F2, T1, lane, r);
+                bn3_rows<MQ>(coef, F2, r, xh);
+            }
 #pragma unroll
             for (int j = 0; j < F2MAX; ++j) {
                 if (j < F2) {

@@ -418,7 +418,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
 }
 
 // ================================================================================================
-// Pass B: forward to d2, E1/E2 (pooled ELU' sums for the BN2 backward), BN3 statistics.  v comes
+// Pass B: forward to d2, E1/E2 (pooled ELU' sums for the BN2 backward), BN3 statistics; the block-2
+// depthwise and pointwise outputs q, r go to their planes for passes C and D.  v comes
 // from pass A's v plane (no spatial GEMM, no FIR here): the pass streams 16 KB of v per trial in and
 // 12 KB of d2 / E1 / E2 out, with one workgroup barrier per trial.
 // part row: [Sr F2][Sr2 F2]
@@ -430,7 +431,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
                                                       const float* __restrict__ vg,
                                                       const uint8_t* __restrict__ mask2,
                                                       float* __restrict__ d2g, float* __restrict__ E1g,
-                                                      float* __restrict__ E2g, float* __restrict__ part,
+                                                      float* __restrict__ E2g, float* __restrict__ q3g,
+                                                      float* __restrict__ r3g, float* __restrict__ part,
                                                       FinArgs fa, FoldCall fc) {
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 1, TR_ENTRY);
@@ -443,6 +445,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         vg = (const float*)(ws + fc.off.v);
         mask2 = nullptr;
         d2g = (float*)(ws + fc.off.d2); E1g = (float*)(ws + fc.off.E1); E2g = (float*)(ws + fc.off.E2);
+        q3g = (float*)(ws + fc.off.q3); r3g = (float*)(ws + fc.off.r3);
         part = (float*)(ws + fc.off.partB);
         fa = fold_fin(fc, f, TK_B, 1, 0, true, false, g.nparam);
         dk0 = fold_drop_key(fc, f, 0);
@@ -545,6 +548,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 #pragma unroll
                     for (int k = 0; k < K2; ++k) a = fmaf(w2[k], dr[t + k], a);
                     Qs[o * RS2 + t] = a;
+                    q3g[((size_t)b * F2 + o) * T1 + t] = a;       // q plane (pass D)
                 }
             }
         }
@@ -584,6 +588,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
                     float rr = 0.f;
 #pragma unroll
                     for (int i = 0; i < F2MAX; ++i) rr = fmaf(w3[i], qv[i], rr);
+                    r3g[((size_t)b * F2 + o) * T1 + t] = rr;      // r plane (passes C, D)
                     sr[r] += rr;
                     sr2[r] = fmaf(rr, rr, sr2[r]);
                 }
