@@ -37,9 +37,10 @@ def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
     """Per-trial algorithmic FLOPs (MAC x 2) and HBM bytes of each pass kernel as implemented
     (DESIGN.md section 4).  Returns {kernel: (flop, bytes)}.  Pass A writes the s and v planes
     ([F2, T] fp32 each) that pass B (v) and pass E (s, v) read instead of recomputing the spatial
-    GEMM and the FIR."""
+    GEMM and the FIR; pass B writes the block-2 q and r planes that passes C (r) and D (q, r) read
+    instead of recomputing the depthwise and pointwise convolutions."""
     F2 = F1 * D
-    T1, T2 = T // 4, T // 128
+    T1, T2 = T // 4, T // 32          # pooled lengths: T/4 (block 1), T/32 (block 2)
     npairs = K1 * (K1 - 1) // 2
     sp = F2 * C * T                  # spatial GEMM
     fir = F2 * T * K1                # one 32-tap FIR over the F2 rows
@@ -49,9 +50,9 @@ def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
     sv = F2 * ((T + 7) // 8 * 8) * 4  # one s / v plane row block of a trial
     return {
         "k_pass_a": (2 * (sp + fir + C * T * K1 + 2 * C * npairs), xb + 2 * sv),
-        "k_pass_b": (2 * b2, sv + 3 * row),
-        "k_pass_c": (2 * (b2 + 2 * 4 * F2 * T2), row + 16),
-        "k_pass_d": (2 * (b2 + 2 * F2 * F2 * T1 + 2 * F2 * T1 * 16), 4 * row + 16),
+        "k_pass_b": (2 * b2, sv + 5 * row),                        # + q, r planes out
+        "k_pass_c": (2 * (2 * 4 * F2 * T2), row + 16),               # r plane in: BN3 + head only
+        "k_pass_d": (2 * (2 * F2 * F2 * T1 + 2 * F2 * T1 * 16), 6 * row + 16),   # d2, q, r, E1, E2 in
         "k_pass_e": (2 * (2 * fir + sp), xb + 2 * sv + row),
     }
 
@@ -61,7 +62,7 @@ def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
     once per streaming pass that reads it (the o-chunk workgroups of a trial share it through L2);
     pass A writes the s / v planes, pass B reads v, pass E reads s and v."""
     F2 = F1 * D
-    T1, T2 = T // 4, T // 128
+    T1, T2 = T // 4, T // 32          # pooled lengths: T/4 (block 1), T/32 (block 2)
     npairs = K1 * (K1 - 1) // 2
     sp = F2 * C * T
     fir = F2 * T * K1
