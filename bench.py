@@ -60,7 +60,8 @@ def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
 def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
     """The same for the F2 > 16 passes (csrc/eegnet_wide.hip, cfg5).  Bytes: x is read from HBM
     once per streaming pass that reads it (the o-chunk workgroups of a trial share it through L2);
-    pass A writes the s / v planes, pass B reads v, pass E reads s and v."""
+    pass A writes the s / v planes, pass B reads v, pass E reads s and v; pass B2 writes the q / r
+    planes, pass C reads r, pass D reads q and r."""
     F2 = F1 * D
     T1, T2 = T // 4, T // 32          # pooled lengths: T/4 (block 1), T/32 (block 2)
     npairs = K1 * (K1 - 1) // 2
@@ -73,9 +74,9 @@ def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
     return {
         "k_wpass_a": (2 * (sp + fir + C * T * K1 + 2 * C * npairs), xb + 2 * sv),
         "k_wpass_b": (0, sv + 3 * row),
-        "k_wpass_b2": (2 * b2, row),
-        "k_wpass_c": (2 * (b2 + 2 * 4 * F2 * T2), row + 16),
-        "k_wpass_d": (2 * (b2 + 2 * F2 * F2 * T1 + 2 * F2 * T1 * 16), 4 * row + 16),
+        "k_wpass_b2": (2 * b2, 3 * row),
+        "k_wpass_c": (2 * (2 * 4 * F2 * T2), row + 16),
+        "k_wpass_d": (2 * (2 * F2 * F2 * T1 + 2 * F2 * T1 * 16), 6 * row + 16),
         "k_wpass_e": (2 * (2 * fir + sp), xb + 2 * sv + row),
     }
 

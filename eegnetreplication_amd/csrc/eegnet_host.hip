@@ -51,7 +51,7 @@ static void b2_lds(Geo* g, int nw) {
     const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables
     const int TQ1 = (g->T1 + 3) / 4;
     g->ldsWB2 = std::max(b2 + nw * 2 * 16, tailw(g->nB, 0));
-    g->ldsWC = std::max(b2 + nf4 + nw * 4 + nw * 2 * 16 + g->F2P * g->RB, tailw(g->nC, 0));
+    g->ldsWC = std::max(nf4 + nw * 4 + nw * 2 * 16 + g->F2P * g->RB, tailw(g->nC, 0));    // H | sums | XH
     g->ldsWD = std::max(b2 + g->F2P * g->RB + nf4 + 2 * g->F2 * TQ1, tailw(g->nD, 0));
 }
 
@@ -225,8 +225,8 @@ static WsLayout make_layout(const Geo& g) {
     L.v = take((size_t)g.B * g.F2 * ((g.T + 7) / 8 * 8) * 4);
     // F2 <= 16: pass B's block-2 depthwise output q and pointwise output r [B][F2][T/4], read by passes
     // C (r) and D (q, r) instead of recomputing them from d2
-    L.q3 = take(g.wide ? 0 : per);
-    L.r3 = take(g.wide ? 0 : per);
+    L.q3 = take(per);
+    L.r3 = take(per);
     L.total = o;
     return L;
 }
@@ -360,7 +360,8 @@ static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const flo
                                       (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2),
                                       (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
     { PROF(KID_WB2); hipLaunchKernelGGL(k_wpass_b2<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
-                                      (const float*)(ws + L.d2), (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
+                                      (const float*)(ws + L.d2), (float*)(ws + L.q3), (float*)(ws + L.r3),
+                                      (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
     return 0;
 }
 
@@ -388,12 +389,13 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
         else hipLaunchKernelGGL(k_coltail<5>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
     };
     { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
-                                      (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
+                                      (const float*)(ws + L.r3), m3, dlogits, labels, logits, (float*)(ws + L.dl),
                                       (float*)(ws + L.partC), c_mode, fc, FoldCall{}); } LAUNCH_CHECK("k_wpass_c(bwd)");
     if (g.splitC) { coltail(3, (const float*)(ws + L.partC), g.grid, g.nC, fc, 0); LAUNCH_CHECK("k_coltail(C)"); }
     { PROF(KID_WD); hipLaunchKernelGGL(k_wpass_d<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
                                       (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
-                                      m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
+                                      (const float*)(ws + L.q3), (const float*)(ws + L.r3), m2, m3, dl,
+                                      (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
     LAUNCH_CHECK("k_wpass_d");
     if (g.splitD) { coltail(4, (const float*)(ws + L.partD), g.grid, g.nD, fd, 0); LAUNCH_CHECK("k_coltail(D)"); }
     { PROF(KID_WE); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
@@ -460,20 +462,22 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     if (use_b2_narrow(g)) {
         { PROF(KID_C);
           if (fc.folds) hipLaunchKernelGGL((k_wpass_c<256, true>), dim3(g.gridB2, nf), dim3(256), g.ldsWC * 4, s, g,
-                                           params, coef, (const float*)(ws + L.d2), m3, dlogits, labels, logits,
+                                           params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits,
                                            (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc);
           else hipLaunchKernelGGL((k_wpass_c<256>), dim3(g.gridB2), dim3(256), g.ldsWC * 4, s, g, params, coef,
-                                  (const float*)(ws + L.d2), m3, dlogits, labels, logits, (float*)(ws + L.dl),
+                                  (const float*)(ws + L.r3), m3, dlogits, labels, logits, (float*)(ws + L.dl),
                                   (float*)(ws + L.partC), c_mode, fcC, fc);
         } LAUNCH_CHECK("k_wpass_c<256>");
         { PROF(KID_D);
           if (fc.folds) hipLaunchKernelGGL((k_wpass_d<256, true>), dim3(g.gridB2, nf), dim3(256), g.ldsWD * 4, s, g,
                                            params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1),
-                                           (const float*)(ws + L.E2), m2, m3, dl, (float*)(ws + L.dp2),
+                                           (const float*)(ws + L.E2), (const float*)(ws + L.q3),
+                                           (const float*)(ws + L.r3), m2, m3, dl, (float*)(ws + L.dp2),
                                            (float*)(ws + L.partD), fd, fc);
           else hipLaunchKernelGGL((k_wpass_d<256>), dim3(g.gridB2), dim3(256), g.ldsWD * 4, s, g, params, coef,
                                   (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
-                                  m2, m3, dl, (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, fc);
+                                  (const float*)(ws + L.q3), (const float*)(ws + L.r3), m2, m3, dl,
+                                  (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, fc);
         } LAUNCH_CHECK("k_wpass_d<256>");
     } else {
     { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
@@ -614,7 +618,7 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     memset(&none, 0, sizeof(none));
     if (g.wide) {
         { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params,
-                                          (const float*)(w + L.coef), (const float*)(w + L.d2), mask3,
+                                          (const float*)(w + L.coef), (const float*)(w + L.r3), mask3,
                                           (const float*)nullptr, (const int64_t*)nullptr, logits, (float*)nullptr,
                                           (float*)nullptr, (int)PC_LOGITS, none, FoldCall{}); }
         LAUNCH_CHECK("k_wpass_c(fwd)");

@@ -415,6 +415,33 @@ __device__ __forceinline__ void b2_stage(const float* __restrict__ src, int F2, 
     }
 }
 
+// the inverse: padded LDS rows [F2P][RB] -> trial b's [F2][T1] rows of a global plane
+__device__ __forceinline__ void b2_put(const float* src, int F2, int T1, int RB, float* __restrict__ dst, int tid,
+                                       int nth) {
+    const int n = F2 * T1;
+    if ((T1 & 3) == 0) {
+        const int TQ1 = T1 >> 2;
+        for (int i = tid; i < n / 4; i += nth) {
+            const int o = i / TQ1, q = i - o * TQ1;
+            const floatx4 v = lds_ld4(src + o * RB + LQW + 4 * q);
+            reinterpret_cast<float4*>(dst)[i] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    } else {
+        for (int i = tid; i < n; i += nth) {
+            const int o = i / T1, t = i - o * T1;
+            dst[i] = src[o * RB + LQW + t];
+        }
+    }
+}
+
+// one 16 x 16 MFMA-layout tile (rows 16 jt + 4 (lane >> 4) + r, column 16 n + (lane & 15)) into
+// padded LDS rows [F2P][RB]
+__device__ __forceinline__ void tile_lds(float* dst, const floatx4& a, int RB, int jt, int n, int lane) {
+    float* p = dst + (16 * jt + 4 * (lane >> 4)) * RB + LQW + 16 * n + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r * RB] = a[r];
+}
+
 // q[o][t] = sum_k w2[o][k] d2[o][t + k - 7] (model.py:54-61, 'same', pad 7 | 8) for every row and
 // 4-sample quad: windows of 24 floats from the padded rows (start t - 8), taps from an LDS table
 __device__ __forceinline__ void b2_dw16(const float* D2, const float* W2s, float* Q, int F2, int T1, int RB,
@@ -485,13 +512,14 @@ __device__ __forceinline__ void load_w2s(const Geo& g, const float* __restrict__
 constexpr int NTTW = 8;
 
 // ================================================================================================
-// Wide pass B2: BN3 (model.py:71) batch statistics.  Partial row [Sr F2][Sr2 F2].
+// Wide pass B2: block 2's depthwise and pointwise convolutions -> the q and r planes (read by passes
+// C and D) and BN3 (model.py:71) batch statistics.  Partial row [Sr F2][Sr2 F2].
 // LDS: D2 [F2P][RB] | Q [F2P][RB] | W2s [F2P][16] | wave sums [NWB2][2][16]
 // ================================================================================================
 template <int NT>
 __global__ __launch_bounds__(NT) void k_wpass_b2(Geo g, const float* __restrict__ prm,
-                                                   const float* __restrict__ d2g, float* __restrict__ part,
-                                                   FinArgs fa) {
+                                                   const float* __restrict__ d2g, float* __restrict__ q3g,
+                                                   float* __restrict__ r3g, float* __restrict__ part, FinArgs fa) {
     const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, RB = g.RB, NJT = F2P >> 4;
     const int NT1 = (T1 + 15) >> 4;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -515,16 +543,21 @@ __global__ __launch_bounds__(NT) void k_wpass_b2(Geo g, const float* __restrict_
         __syncthreads();
         b2_dw16(D2, W2s, Q, F2, T1, RB, tid, NT);
         __syncthreads();
+        const size_t rb = (size_t)b * F2 * T1;
         floatx4 acc[NTTW];
         b2_pw<NTTW>(Q, W3s, F2P, NT1, RB, mp, acc, lane);
 #pragma unroll
         for (int i = 0; i < NTTW; ++i) {
-            const int t = 16 * (mp.n0 + mp.dn * i) + li;
+            const int n = mp.n0 + mp.dn * i, t = 16 * n + li;
+            if (n < NT1) tile_lds(D2, acc[i], RB, mp.jt, n, lane);          // d2 rows are dead
             if (t < T1) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) { sr[r] += acc[i][r]; sr2[r] = fmaf(acc[i][r], acc[i][r], sr2[r]); }
             }
         }
+        __syncthreads();                                   // r rows complete
+        b2_put(Q, F2, T1, RB, q3g + rb, tid, NT);
+        b2_put(D2, F2, T1, RB, r3g + rb, tid, NT);
         __syncthreads();                                   // D2 / Q free for the next trial
     }
     // rows 16 jt + 4 lk + r: sums over the 16 lanes li, then over the waves sharing jt
@@ -567,13 +600,13 @@ __device__ __forceinline__ void b2_bn3(const float* coef, const B2Map& mp, float
 }
 
 // ================================================================================================
-// Wide pass C: head (model.py:71-84).  logits, and (PC_BWD) CE, classifier grads, BN3-bwd sums.
-// Partial row [dWfc 4*NF][dbfc 4][Sdz3 F2][Sdz3x F2][loss].
-// LDS: D2 | Q | W2s | H [NF] (features, then their gradients) | class partials [(NT / 64)][4] | sums
+// Wide pass C: head (model.py:71-84) from the r plane of pass B2 (or narrow pass B).  logits, and
+// (PC_BWD) CE, classifier grads, BN3-bwd sums.  Partial row [dWfc 4*NF][dbfc 4][Sdz3 F2][Sdz3x F2][loss].
+// LDS: H [NF] (features, then their gradients) | class partials [(NT / 64)][4] | sums | XH [F2P][RB]
 // ================================================================================================
 template <int NT, bool FOLD = false>
 __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__ prm, const float* coef,
-                                                  const float* __restrict__ d2g, const uint8_t* __restrict__ mask3,
+                                                  const float* __restrict__ r3g, const uint8_t* __restrict__ mask3,
                                                   const float* __restrict__ dlin, const int64_t* __restrict__ labels,
                                                   float* __restrict__ logits, float* __restrict__ dlout,
                                                   float* __restrict__ part, int mode, FinArgs fa, FoldCall fc) {
@@ -585,7 +618,7 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
-        d2g = (const float*)(ws + fc.off.d2);
+        r3g = (const float*)(ws + fc.off.r3);
         mask3 = nullptr; dlin = nullptr; logits = nullptr;
         labels = f.labels + fc.row0;
         dlout = (float*)(ws + fc.off.dl);
@@ -596,21 +629,15 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
         dk1 = drop_key(g, 1);
     }
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* D2 = sm;
-    float* Q = D2 + F2P * RB;
-    float* W2s = Q + F2P * RB;
-    float* W3s = W2s + F2P * K2;
-    float* H = W3s + F2P * (F2P + 1);
+    float* H = sm;
     float* lgs = H + ((NF + 3) & ~3);
     float* ws_ = lgs + (NT / 64) * 4;
     float* XH = ws_ + (NT / 64) * 2 * 16;                   // BN3-normalised r [F2P][RB] (t at LQW + t)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    for (int i = tid; i < 2 * F2P * RB; i += NT) sm[i] = 0.f;
-    load_w2s(g, prm, W2s, F2P, tid, NT);
-    stage_w3(g, prm, W3s, F2P, tid, NT);
     const B2Map mp = b2_map(NJT, wave, NT / 64);
+    for (int i = tid; i < F2P * RB; i += NT) XH[i] = 0.f;
     float g3[4], b3[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -635,9 +662,7 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid, NT);
-        __syncthreads();
-        b2_dw16(D2, W2s, Q, F2, T1, RB, tid, NT);
+        b2_stage(r3g + (size_t)b * F2 * T1, F2, T1, RB, XH, tid, NT);       // r rows (pass B / B2)
         __syncthreads();
         {
             float mu[4], inv[4];
@@ -647,17 +672,16 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
                 mu[r] = coef[CF_MU3 * CSTR + jj];
                 inv[r] = coef[CF_INV3 * CSTR + jj];
             }
-            // per time tile: pointwise (MFMA) -> BN3 -> XH; ELU -> AvgPool(1,8) -> H (flattened
-            // index j*T2 + t/8, model.py:75)
+            // per time tile: BN3 -> XH (in place over r); ELU -> AvgPool(1,8) -> H (flattened index
+            // j*T2 + t/8, model.py:75)
             for (int i = 0; i < NTTW; ++i) {
                 const int n = mp.n0 + mp.dn * i;
                 if (n >= NT1) break;
-                const floatx4 acc = b2_pw_tile(Q, W3s, F2P, mp.jt, n, RB, lane);
                 const int t = 16 * n + li;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int jj = 16 * mp.jt + 4 * lk + r;
-                    const float xh = (acc[r] - mu[r]) * inv[r];
+                    const float xh = (XH[jj * RB + LQW + t] - mu[r]) * inv[r];
                     XH[jj * RB + LQW + t] = xh;
                     float e = t < 8 * T2 ? elu_f(fmaf(g3[r], xh, b3[r])) : 0.f;
                     e = sum8_hi(e);
@@ -739,7 +763,7 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
                 }
             }
         }
-        __syncthreads();                                   // H, D2, Q free for the next trial
+        __syncthreads();                                   // H, XH free for the next trial
     }
     if (!(mode & PC_BWD)) return;
     float* row = part + (size_t)blockIdx.x * g.nC;
@@ -778,15 +802,16 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
 }
 
 // ================================================================================================
-// Wide pass D: block_2 backward -- dW3 and dq on the matrix cores, dw2, dd2 -> dropout -> dp2, and
-// the BN2-backward sums from pass B's pooled ELU' sums.  Partial row [dW3 F2*F2][dw2 F2*16][Sdz2 F2]
-// [Sdz2x F2].
+// Wide pass D: block_2 backward from the d2, q and r planes -- dW3 and dq on the matrix cores, dw2,
+// dd2 -> dropout -> dp2, and the BN2-backward sums from pass B's pooled ELU' sums.  Partial row
+// [dW3 F2*F2][dw2 F2*16][Sdz2 F2][Sdz2x F2].
 // LDS: D2 [F2P][RB] | Q [F2P][RB] (q, then dq) | DR [F2P][RB] | W2s | Hd [NF] | item sums
 // ================================================================================================
 template <int NT, bool FOLD = false>
-__global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__ prm, const float* coef,
+__global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo g, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ d2g, const float* __restrict__ E1g,
-                                                  const float* __restrict__ E2g, const uint8_t* __restrict__ mask2,
+                                                  const float* __restrict__ E2g, const float* __restrict__ q3g,
+                                                  const float* __restrict__ r3g, const uint8_t* __restrict__ mask2,
                                                   const uint8_t* __restrict__ mask3, const float* __restrict__ dl,
                                                   float* __restrict__ dp2g, float* __restrict__ part, FinArgs fa,
                                                   FoldCall fc) {
@@ -800,6 +825,7 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
         coef = (const float*)(ws + fc.off.coef);
         d2g = (const float*)(ws + fc.off.d2);
         E1g = (const float*)(ws + fc.off.E1); E2g = (const float*)(ws + fc.off.E2);
+        q3g = (const float*)(ws + fc.off.q3); r3g = (const float*)(ws + fc.off.r3);
         mask2 = nullptr; mask3 = nullptr;
         dl = (const float*)(ws + fc.off.dl);
         dp2g = (float*)(ws + fc.off.dp2);
@@ -857,7 +883,10 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
         float dlv[NCLS];
 #pragma unroll
         for (int n = 0; n < NCLS; ++n) dlv[n] = dl[(size_t)b * NCLS + n];
-        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid, NT);
+        const size_t rb = (size_t)b * F2 * T1;
+        b2_stage(d2g + rb, F2, T1, RB, D2, tid, NT);
+        b2_stage(q3g + rb, F2, T1, RB, Q, tid, NT);
+        b2_stage(r3g + rb, F2, T1, RB, DR, tid, NT);      // r rows, then dr in place
         // dh -> dropout -> dp3 (flattened) into Hd
 #pragma unroll
         for (int u = 0; u < MAXNFW; ++u) {
@@ -867,8 +896,6 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
             for (int n = 0; n < NCLS; ++n) d = fmaf(dlv[n], wf[n][u], d);
             if (f < NF) Hd[f] = d * keep_mul(g, mask3, dk1, (unsigned)(b * NF + f));
         }
-        __syncthreads();
-        b2_dw16(D2, W2s, Q, F2, T1, RB, tid, NT);
         __syncthreads();
         {   // BN3 backward (finalize 3's batch constants): dr = A3 dz3 + B3 + C3 xh3 -> DR rows
             float mu[4], inv[4];
@@ -881,12 +908,11 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
             for (int i = 0; i < NTTW; ++i) {
                 const int n = mp.n0 + mp.dn * i;
                 if (n >= NT1) break;
-                const floatx4 acc = b2_pw_tile(Q, W3s, F2P, mp.jt, n, RB, lane);
                 const int t = 16 * n + li;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int jj = 16 * mp.jt + 4 * lk + r;
-                    const float xh = (acc[r] - mu[r]) * inv[r];
+                    const float xh = (DR[jj * RB + LQW + t] - mu[r]) * inv[r];
                     const float dz = (t < 8 * T2 && jj < F2)
                                          ? Hd[jj * T2 + (t >> 3)] * 0.125f * elu_d(fmaf(g3[r], xh, b3[r])) : 0.f;
                     const float d = (t < T1 && jj < F2) ? fmaf(A3[r], dz, fmaf(C3[r], xh, B3[r])) : 0.f;
@@ -943,7 +969,6 @@ __global__ __launch_bounds__(NT) void k_wpass_d(Geo g, const float* __restrict__
             }
         }
         // dd2[t] = sum_k w2[k] dq[t + 7 - k] -> dropout -> dp2; BN2-backward sums (E1 / E2 of pass B)
-        const size_t rb = (size_t)b * F2 * T1;
         for (int it = tid; it < nit; it += NT) {
             const int o = it / TQ1, qd = it - o * TQ1;
             float s1 = 0.f, s2 = 0.f;
