@@ -32,18 +32,30 @@ __device__ __forceinline__ int fir_oct(int lane) { return (lane & 7) | ((lane >>
 
 // x staging by LDS-DMA (global_load_lds_dwordx4: no VGPR destination, the wave's 64 lanes write
 // 1 KiB contiguously): one wave-instruction per 256-sample piece of a channel row, rows dealt
-// round-robin over the waves.  Used when T is a multiple of 256 (16-byte aligned, whole pieces);
-// other shapes stage through registers (x_prefetch / x_store).  The DMA is issued right after the
+// round-robin over the waves.  Used by the compile-time shapes (22 x 256 and 22 x 257); the
+// runtime-shape kernels stage through registers (x_prefetch / x_store).  The DMA is issued right after the
 // last reader of the x buffer and drains at the next __syncthreads() (the compiler's vmcnt(0)).
 typedef __attribute__((address_space(1))) void gvoid_t;
 typedef __attribute__((address_space(3))) void lvoid_t;
+// Rows of other lengths (22 x 257, the real recordings) go by 4-byte pieces: 64 samples per wave
+// instruction, the row's last piece on its first T mod 64 lanes only (the pads stay zero).
 __device__ __forceinline__ void x_dma(const float* __restrict__ xb, int C, int T, int RS, int LP, float* Xs,
                                       int wave, int lane) {
-    const int np = T >> 8;                             // 256-sample pieces per row
-    for (int i = wave; i < C * np; i += NWB) {
-        const int c = i / np, p = i - c * np;
-        __builtin_amdgcn_global_load_lds((gvoid_t*)(xb + (size_t)c * T + 256 * p + 4 * lane),
-                                         (lvoid_t*)(Xs + c * RS + LP + 256 * p), 16, 0, 0);
+    if ((T & 255) == 0) {
+        const int np = T >> 8;                         // 256-sample pieces per row
+        for (int i = wave; i < C * np; i += NWB) {
+            const int c = i / np, p = i - c * np;
+            __builtin_amdgcn_global_load_lds((gvoid_t*)(xb + (size_t)c * T + 256 * p + 4 * lane),
+                                             (lvoid_t*)(Xs + c * RS + LP + 256 * p), 16, 0, 0);
+        }
+    } else {
+        const int np = (T + 63) >> 6;                  // 64-sample pieces per row
+        for (int i = wave; i < C * np; i += NWB) {
+            const int c = i / np, p = i - c * np;
+            if (lane < T - 64 * p)
+                __builtin_amdgcn_global_load_lds((gvoid_t*)(xb + (size_t)c * T + 64 * p + lane),
+                                                 (lvoid_t*)(Xs + c * RS + LP + 64 * p), 4, 0, 0);
+        }
     }
 }
 
@@ -64,10 +76,18 @@ __device__ __forceinline__ void dma4(const float* gsrc, const float* ldst) {    
 }
 __device__ __forceinline__ void x_dma_asm(const float* __restrict__ xb, int C, int T, int RS, int LP, float* Xs,
                                           int wave, int lane) {
-    const int np = T >> 8;
-    for (int i = wave; i < C * np; i += NWB) {
-        const int c = i / np, p = i - c * np;
-        dma16(xb + (size_t)c * T + 256 * p + 4 * lane, Xs + c * RS + LP + 256 * p);
+    if ((T & 255) == 0) {
+        const int np = T >> 8;
+        for (int i = wave; i < C * np; i += NWB) {
+            const int c = i / np, p = i - c * np;
+            dma16(xb + (size_t)c * T + 256 * p + 4 * lane, Xs + c * RS + LP + 256 * p);
+        }
+    } else {
+        const int np = (T + 63) >> 6;
+        for (int i = wave; i < C * np; i += NWB) {
+            const int c = i / np, p = i - c * np;
+            if (lane < T - 64 * p) dma4(xb + (size_t)c * T + 64 * p + lane, Xs + c * RS + LP + 64 * p);
+        }
     }
 }
 __device__ __forceinline__ void flat_dma_asm(const float* __restrict__ src, int n, float* dst, int wave, int lane) {
@@ -243,7 +263,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
             ea[i] = -2;                                  // unused slot
         }
     }
-    constexpr bool XDMA = TT && (TT % 256 == 0);
+    constexpr bool XDMA = TT != 0;                    // compile-time shapes: x / s rows by LDS-DMA
     float pf[XDMA ? 1 : PF];
     if constexpr (XDMA) {
         if (b0 < b1) x_dma(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
@@ -654,7 +674,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     int b0, b1;
     trial_range(g, b0, b1);
     const int li = lane & 15, lk = lane >> 4;
-    constexpr bool XDMA = TT && (TT % 256 == 0);
+    constexpr bool XDMA = TT != 0;                    // compile-time shapes: x / s rows by LDS-DMA
     static_assert(!XDMA || (CC && FF), "LDS-DMA staging is specialised to compile-time C and F2");
 
     TRACE_PS(g, 0);
@@ -678,8 +698,11 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     // specialised shapes with one octet per lane and every row live: e overwrites the dy rows in place;
     // otherwise e goes to the s rows
     constexpr bool ONEOC = FF && TT && (EEG_NO(TT) <= 32) && (FF == RPW * NWB);
-    float* const Eb = ONEOC ? Dys : Ss;
-    constexpr bool XDMA_ = TT && (TT % 256 == 0);
+    // with the s rows staged by DMA (the next trial's land during the dws GEMM) e must not go to them:
+    // it overwrites the dy rows in place, from registers once every read of the row is done
+    constexpr bool EINPL = ONEOC || XDMA;
+    float* const Eb = EINPL ? Dys : Ss;
+    constexpr bool XDMA_ = TT != 0;
     constexpr bool DPDMA_ = XDMA_ && FF && ((FF * (TT / 4)) % 256 == 0);
     // the specialised pipeline (EEGNet-8,2 at T = 256): every wave DMAs its own rows of the next
     // trial's dp2 (right after its dy2 phase) and s (right after its lag correlation), the next v is
@@ -741,7 +764,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     const int ndp = F2 * T1;
     float pdp[NDP];
     // specialised shapes: dp2 rows go straight to LDS by DMA (no registers, no exposed load)
-    constexpr bool DPDMA = TT && (TT % 256 == 0) && FF && ((FF * (TT / 4)) % 256 == 0);
+    constexpr bool DPDMA = TT && FF && ((FF * (TT / 4)) % 256 == 0);
     if (b0 < b1) {
         if constexpr (XDMA) x_dma(sg + (size_t)b0 * F2 * T, F2, T, RS, LP, Ss, wave, lane);
         else s_rows_load(b0);
@@ -902,6 +925,38 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                         }
                     }
                 }
+                if constexpr (EINPL) {                     // e over this wave's dy rows (MO octets per lane)
+                    float e[MO][8];
+                    if (oh < F2) {
+                        const float* dyr = Dys + oh * RS;
+#pragma unroll
+                        for (int m = 0; m < MO; ++m) {
+                            const int oc = min(fir_oct(lane) + 32 * m, NO - 1);
+                            float w[4 * G_::NW8];
+                            lds_window<G_::NW8>(dyr + 8 * oc, w);
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) e[m][i] = 0.f;
+#pragma unroll
+                            for (int k = 0; k < K1; ++k)
+#pragma unroll
+                                for (int i = 0; i < 8; ++i) e[m][i] = fmaf(tl[K1 - 1 - k], w[G_::OFFD + i + k], e[m][i]);
+                        }
+                    }
+                    wave_lds_fence();                      // every dy / s read of this wave is done
+                    if (oh < F2) {
+                        float* erow = Dys + oh * RS + LP;
+#pragma unroll
+                        for (int m = 0; m < MO; ++m) {
+                            const int oc = fir_oct(lane) + 32 * m;
+                            if (oc < NO) {
+#pragma unroll
+                                for (int i = 0; i < 8; ++i) e[m][i] = (8 * oc + i < T) ? e[m][i] : 0.f;
+                                lds_st4(erow + 8 * oc, (floatx4){e[m][0], e[m][1], e[m][2], e[m][3]});
+                                lds_st4(erow + 8 * oc + 4, (floatx4){e[m][4], e[m][5], e[m][6], e[m][7]});
+                            }
+                        }
+                    }
+                } else
                 // e -> this wave's s rows (the lag correlation above was their last reader; a wave's
                 // LDS reads and writes stay in order)
                 if (oh < F2) {

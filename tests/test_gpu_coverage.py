@@ -63,15 +63,17 @@ def _check_step(model, x_np, y_np, p, masks, what, loss_scale=1.0):
 # ---------------------------------------------------------------------------------------------
 # dropout generator
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("p,T", [(0.5, 256), (0.25, 257)])
-def test_dropout_generator_step_matches_oracle(p, T):
+@pytest.mark.parametrize("p,T,B", [(0.5, 256, 64), (0.25, 257, 64), (0.25, 257, 800)])
+def test_dropout_generator_step_matches_oracle(p, T, B):
     """Train-mode forward + CE-in-backward with masks drawn ON THE DEVICE for (seed, offset), against
     the float64 oracle given the masks the numpy restatement of the generator draws: logits, loss,
     grads and running statistics agree, so forward and backward used the same masks, the keep
-    factor is 1/(1-p), and the device indices (b*F2+o)*T1+q / b*NF+i are the ones restated."""
+    factor is 1/(1-p), and the device indices (b*F2+o)*T1+q / b*NF+i are the ones restated.
+    B = 800 at 22 x 257 gives the streaming passes' workgroups several trials each (the LDS-DMA
+    prefetch of the next trial's x / s / dp2 rows)."""
     from eegnetreplication_amd import ops
     dev = _dev()
-    B, C = 64, 22
+    C = 22
     m = random_model(C, T, p=p, seed=int(100 * p) + T)
     x_np, y_np = make_inputs(B, C, T, 31)
     seed, offset = 0x1234_5678_9ABC, 17
