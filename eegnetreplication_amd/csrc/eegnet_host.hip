@@ -55,15 +55,16 @@ static void b2_lds(Geo* g, int nw) {
     g->ldsWD = std::max(b2 + g->F2P * g->RB + nf4 + 2 * g->F2 * TQ1, tailw(g->nD, 0));
 }
 
-// Block-2 passes C / D of the F2 <= 16 step: one trial per wave (k_pass_c / k_pass_d, the better
-// choice at large batches: B = 4096 runs them in 32 / 50 us against 68 / 83 us) or whole-trial
-// 256-thread workgroups (the wide path's k_wpass_c / k_wpass_d: more workgroups, so the better
-// choice at small per-launch grids, e.g. batch 64 and fold-indexed launches).  EEGNET_B2=0/1 forces.
-static bool use_b2_narrow(const Geo& g) {
+// Block-2 passes C / D of the F2 <= 16 step: one trial per wave (k_pass_c / k_pass_d, the default)
+// or whole-trial 256-thread workgroups (the wide path's k_wpass_c / k_wpass_d, EEGNET_B2=1).  Before
+// pass B stored the q / r planes the whole-trial kernels won at small per-launch grids (batch 64,
+// fold-indexed launches); with the planes the one-trial-per-wave kernels win the fold-indexed
+// real-protocol leg (6.5 M against 5.9 M trials/s) and lose 3-7% on a lone batch of 64.  One rule
+// for every launch keeps a fold-indexed step bit-identical to the same fold's FusedTrainer step.
+static bool use_b2_narrow(const Geo&) {
     static int v = -2;
-    if (v == -2) { const char* e = getenv("EEGNET_B2"); v = e ? (e[0] == '1' ? 1 : 0) : -1; }
-    if (v >= 0) return v == 1;
-    return g.gridB2 < 4 * device_cus() / 2;     // small batches (e.g. the protocols' 64): more workgroups
+    if (v == -2) { const char* e = getenv("EEGNET_B2"); v = e ? (e[0] == '1' ? 1 : 0) : 0; }
+    return v == 1;
 }
 
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
