@@ -324,8 +324,9 @@ def main():
     ap.add_argument("--no-infer", action="store_true", help="skip the cfg5 bf16 inference leg")
     ap.add_argument("--infer-batch", type=int, default=16384)
     ap.add_argument("--no-folds", action="store_true", help="skip the fold-batched real-protocol leg")
-    ap.add_argument("--folds", type=int, default=45,
-                    help="folds of the real-protocol leg (45: one GPU's balanced half of the 90 cross-subject folds)")
+    ap.add_argument("--folds", type=int, default=90,
+                    help="folds of the real-protocol leg (90: the cross-subject protocol's folds, one fold batch "
+                         "at the CLI's --fold-batch 90)")
     ap.add_argument("--nx", type=int, default=4, help="distinct x buffers rotated in the timed region")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 EEGNet-16,4 training leg")
     ap.add_argument("--cfg5-batch", type=int, default=1024)

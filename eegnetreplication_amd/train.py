@@ -349,7 +349,7 @@ def main(argv=None) -> None:
     ap.add_argument("--generateReport", type=bool, default=True, help="Generate report after training.")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", type=str, default=".", help="directory for models/ and reports/")
-    ap.add_argument("--fold-batch", type=int, default=48,
+    ap.add_argument("--fold-batch", type=int, default=90,
                     help="train up to this many folds together on one GPU (FoldBatch, balanced batches); "
                          "0/1: one at a time")
     ap.add_argument("--max-units", type=int, default=0,

@@ -137,7 +137,7 @@ def test_device_loader_matches_dataloader_shuffle():
 
 
 def test_fold_batches_are_balanced(monkeypatch):
-    """_run_units splits the units into balanced fold batches of at most fold_batch (90 at 48: 45 + 45),
+    """_run_units splits the units into balanced fold batches of at most fold_batch (90 at 48: 45 + 45, not 48 + 42),
     in unit order, and returns the results in unit order."""
     from eegnetreplication_amd import train as T_
     seen = []
