@@ -345,16 +345,29 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
             if (o < F2) {
                 const float* row = Ss + o * RS;
                 if constexpr (DEFER) {
+                    // 22 x 257: the last octet holds one sample (T - 1 = 256), one 32-tap dot product
+                    constexpr bool TAIL1 = TT && (TT % 8 == 1) && (EEG_NO(TT) % 32 == 1);
 #pragma unroll
                     for (int m = 0; m < MOA; ++m) {
                         const int oc = fir_oct(lane) + 32 * m;
                         if (oc < NO) {
                             float w[4 * G_::NW8];
                             lds_window<G_::NW8>(row + 8 * oc, w);
-                            fir8<K1, G_::OFF>(w, tl, vs[m]);
+                            if (TAIL1 && m == MOA - 1) {
+                                float a = 0.f;
 #pragma unroll
-                            for (int i = 0; i < 8; ++i)
-                                if (8 * oc + i < T) { svl += vs[m][i]; sv2l = fmaf(vs[m][i], vs[m][i], sv2l); }
+                                for (int k = 0; k < K1; ++k) a = fmaf(tl[k], w[G_::OFF + k], a);
+                                vs[m][0] = a;
+#pragma unroll
+                                for (int i = 1; i < 8; ++i) vs[m][i] = 0.f;
+                                svl += a;
+                                sv2l = fmaf(a, a, sv2l);
+                            } else {
+                                fir8<K1, G_::OFF>(w, tl, vs[m]);
+#pragma unroll
+                                for (int i = 0; i < 8; ++i)
+                                    if (8 * oc + i < T) { svl += vs[m][i]; sv2l = fmaf(vs[m][i], vs[m][i], sv2l); }
+                            }
                         }
                     }
                 } else {
@@ -929,6 +942,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                     float e[MO][8];
                     if (oh < F2) {
                         const float* dyr = Dys + oh * RS;
+                        constexpr bool TAIL1 = TT && (TT % 8 == 1) && (EEG_NO(TT) % 32 == 1);
 #pragma unroll
                         for (int m = 0; m < MO; ++m) {
                             const int oc = min(fir_oct(lane) + 32 * m, NO - 1);
@@ -936,10 +950,16 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                             lds_window<G_::NW8>(dyr + 8 * oc, w);
 #pragma unroll
                             for (int i = 0; i < 8; ++i) e[m][i] = 0.f;
+                            if (TAIL1 && m == MO - 1) {            // the last octet: sample T - 1 only
 #pragma unroll
-                            for (int k = 0; k < K1; ++k)
+                                for (int k = 0; k < K1; ++k) e[m][0] = fmaf(tl[K1 - 1 - k], w[G_::OFFD + k], e[m][0]);
+                            } else {
 #pragma unroll
-                                for (int i = 0; i < 8; ++i) e[m][i] = fmaf(tl[K1 - 1 - k], w[G_::OFFD + i + k], e[m][i]);
+                                for (int k = 0; k < K1; ++k)
+#pragma unroll
+                                    for (int i = 0; i < 8; ++i)
+                                        e[m][i] = fmaf(tl[K1 - 1 - k], w[G_::OFFD + i + k], e[m][i]);
+                            }
                         }
                     }
                     wave_lds_fence();                      // every dy / s read of this wave is done
