@@ -173,7 +173,9 @@ __device__ __forceinline__ void half_taps(const float (&tap)[NTS][K1], int hr, f
 }
 
 // Temporal taps of this wave's rows: one shared set for the specialised EEGNet-8,2 shapes (the
-// rows 2w, 2w+1 of a wave are group w when D = 2), one set per row otherwise.
+// rows 2w, 2w+1 of a wave are group w when D = 2), one set per row otherwise.  The taps are
+// wave-uniform: readfirstlane keeps them in SGPRs even when prm comes from a fold record (an ordinary
+// load, whose result the compiler would otherwise hold per lane: K1 VGPRs per tap set).
 template <int K1, int NTS>
 __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict__ prm, int D, int F2, int wave,
                                           float (&tap)[NTS][K1]) {
@@ -182,7 +184,8 @@ __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict_
         const int o = RPW * wave + r;
         const int gg = (o < F2 ? o : 0) / D;
 #pragma unroll
-        for (int k = 0; k < K1; ++k) tap[r][k] = prm[g.o_w1 + gg * K1 + k];
+        for (int k = 0; k < K1; ++k)
+            tap[r][k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prm[g.o_w1 + gg * K1 + k])));
     }
 }
 
