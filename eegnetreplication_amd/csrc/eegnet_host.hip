@@ -290,7 +290,8 @@ static void set_attrs_shape() {
                           (const void*)k_pass_c<K1, CC, TT, FF>, (const void*)k_pass_d<K1, CC, TT, FF>,
                           (const void*)k_pass_e<K1, CC, TT, FF>, (const void*)k_pass_a<K1, CC, TT, FF, true>,
                           (const void*)k_pass_b<K1, CC, TT, FF, true>, (const void*)k_pass_c<K1, CC, TT, FF, true>,
-                          (const void*)k_pass_d<K1, CC, TT, FF, true>, (const void*)k_pass_e<K1, CC, TT, FF, true>})
+                          (const void*)k_pass_d<K1, CC, TT, FF, true>, (const void*)k_pass_e<K1, CC, TT, FF, true>,
+                          (const void*)k_pass_d<K1, CC, TT, FF, false, false>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipFuncSetAttribute((const void*)k_infer<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
@@ -488,7 +489,12 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
                        m2, m3, dl, (float*)(ws + L.dp2), \
                        (float*)(ws + L.partD), fd, fc); \
-    else hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
+    else if (m2 || m3) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
+                       (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
+                       m2, m3, dl, (float*)(ws + L.dp2), \
+                       (float*)(ws + L.partD), fd, fc); \
+    else hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, false, false>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
                        m2, m3, dl, (float*)(ws + L.dp2), \

@@ -344,7 +344,9 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
 // part row: [dW3 F2*F2][dw2 F2*16][Sdz2 F2][Sdz2x F2]
 // Per-wave LDS rows (stride RSW): P0 d2 (pad LPD) | P1 q, then dq (pad LPQ) | P2 dr (pad LPQ) | Hs [NF].
 // ================================================================================================
-template <int K1, int CC, int TT, int FF, bool FOLD = false>
+// MASK = false: dropout from the device generator only (mask2 / mask3 are null).  The host-mask
+// path costs registers in this kernel (256 VGPRs + spills against 156), so it is its own instantiation.
+template <int K1, int CC, int TT, int FF, bool FOLD = false, bool MASK = true>
 __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict__ prm,
                                                  const float* coef,    // the finalize writes it: no __restrict__
                                                  const float* __restrict__ d2g,
@@ -379,6 +381,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
         dk0 = drop_key(g, 0);
         dk1 = drop_key(g, 1);
     }
+    if constexpr (!MASK) { mask2 = nullptr; mask3 = nullptr; }
     constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
     constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
     const int RSW = TT ? row_stride_b2(TT / 4) : g.RSW;
