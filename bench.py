@@ -5,10 +5,13 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Prints ONE JSON line on rank 0.  `value` = trials/s over all ranks (weak scaling: 4096 trials per
-GPU per step; N>1 = data parallel with one RCCL gradient all-reduce per step).  `roofline` is for the
-kernel with the largest device time, from HIP events recorded inside the timed region;
-`cpu_baseline` times the stock-PyTorch CPU restatement of the reference step (oracle/torch_ref.py)
-on this host's cores over a bounded sample.
+GPU per step; N>1 = data parallel with one RCCL all-reduce per step).  `cfg4_dp` is BASELINE
+configs[3] at its own size: global batch 65,536 split over the ranks (strong scaling).  `roofline`
+is for the kernel with the largest device time, from HIP events recorded inside the timed region,
+priced on SURVEY 8(d)'s algorithmic bytes (x reads) and the implemented FLOPs (max of the two
+bounds); `step_roofline` does the same for the whole step.  `cpu_baseline` times the stock-PyTorch
+CPU restatement of the reference step (oracle/torch_ref.py) on this host's cores over bounded
+samples: the cfg2 step and the reference's real loop (batch 64, 22 x 257).
 """
 
 from __future__ import annotations
@@ -31,6 +34,20 @@ PEAK_FP32_TFLOPS = 157.3      # MI355X FP32 dense (vector == matrix on gfx950), 
 PEAK_HBM_GBS = 8000.0         # MI355X HBM3E spec
 REF_FLOP_PER_TRIAL = 6_507_520   # reference formulation, fwd+bwd conv/linear MACx2
 ALG_BYTES_PER_TRIAL = 45_056     # x read twice
+CFG4_GLOBAL_BATCH = 65536        # BASELINE configs[3]
+
+
+def kernel_alg_bytes(C=22, T=256, wide=False):
+    """SURVEY 8(d)'s algorithmic HBM bytes per trial, attributed to the kernels that need them: x
+    is read once for the forward (pass A) and once for the weight gradients (pass E); the labels
+    (8 B) by the CE pass C; every intermediate stays on chip or is recomputed (8(d)'s B_alg
+    45,056 B at 22 x 256).  The planes a kernel chooses to materialise are NOT algorithmic: they
+    show up in its ``impl_bytes`` and in its PMC ``traffic``."""
+    xb = C * T * 4
+    if wide:
+        return {"k_wpass_a": xb, "k_wpass_b": 0, "k_wpass_b2": 0, "k_wpass_c": 8, "k_wpass_d": 0,
+                "k_wpass_e": xb}
+    return {"k_pass_a": xb, "k_pass_b": 0, "k_pass_c": 8, "k_pass_d": 0, "k_pass_e": xb}
 
 
 def kernel_algorithmic(C=22, T=256, F1=8, D=2, K1=32):
@@ -81,20 +98,61 @@ def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
     }
 
 
-def roofline_entry(name, fl, by, avg_s, traffic=None):
-    """Roofline of one kernel from its algorithmic FLOPs / bytes per launch and average duration:
-    FP32 (vector == f32 MFMA on gfx950) when its intensity is above the ridge, else HBM."""
-    ridge = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
-    if fl / by >= ridge:
+def roofline_entry(name, fl, by_alg, by_impl, avg_s, traffic=None):
+    """Roofline of one kernel, SURVEY 8(d): t_F = implemented FLOPs / FP32 peak (vector == f32
+    MFMA on gfx950), t_B = algorithmic bytes (x reads) / HBM peak; the larger is the bound and
+    ``frac`` = that time / the measured average launch.  ``traffic`` = rocprofv3 PMC bytes per launch
+    (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md); its ratio to the algorithmic bytes is the
+    wasted (materialised-plane) traffic."""
+    t_f = fl / (PEAK_FP32_TFLOPS * 1e12)
+    t_b = by_alg / (PEAK_HBM_GBS * 1e9)
+    e = {"kernel": name, "avg_us": round(avg_s * 1e6, 2), "impl_flop_per_launch": fl,
+         "alg_bytes_per_launch": by_alg, "impl_bytes_per_launch": by_impl, "traffic": traffic,
+         "traffic_over_alg": round(traffic / by_alg, 3) if traffic and by_alg else None,
+         "t_fp32_us": round(t_f * 1e6, 2), "t_hbm_us": round(t_b * 1e6, 2)}
+    if t_f >= t_b:
         ach = fl / avg_s / 1e12
-        return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "kernel": name,
-                "avg_us": round(avg_s * 1e6, 2), "alg_flop_per_launch": fl, "alg_bytes_per_launch": by,
-                "note": "fp32 VALU + f32 MFMA share the 157.3 TFLOP/s FP32 peak on gfx950"}
-    ach = by / avg_s / 1e9
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": name,
-            "avg_us": round(avg_s * 1e6, 2), "alg_bytes_per_launch": by}
+        e.update({"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                  "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+                  "note": "FP32 roof: fp32 VALU + f32 MFMA share the 157.3 TFLOP/s FP32 peak on gfx950"})
+    else:
+        ach = by_alg / avg_s / 1e9
+        e.update({"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                  "frac": round(ach / PEAK_HBM_GBS, 4)})
+    # the same launch against the other roof, for reference
+    e["fp32_frac"] = round(t_f / avg_s, 4)
+    e["hbm_frac_alg"] = round(t_b / avg_s, 4)
+    return {k: e[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")} | e
+
+
+def step_roofline(flop_trial, alg_bytes_trial, impl_bytes_trial, trials_per_s, pmc_step_bytes=None,
+                  B=None):
+    """The whole step against SURVEY 8(d): max(B_alg / HBM, F_impl / FP32) per trial over the
+    measured time per trial; plus the step's PMC traffic against B_alg."""
+    t_f = flop_trial / (PEAK_FP32_TFLOPS * 1e12)
+    t_b = alg_bytes_trial / (PEAK_HBM_GBS * 1e9)
+    t = 1.0 / trials_per_s
+    out = {"bound": "mfma" if t_f >= t_b else "hbm", "frac": round(max(t_f, t_b) / t, 4),
+           "fp32_frac": round(t_f / t, 4), "hbm_frac_alg": round(t_b / t, 4),
+           "impl_flop_per_trial": flop_trial, "alg_bytes_per_trial": alg_bytes_trial,
+           "impl_bytes_per_trial": impl_bytes_trial}
+    if pmc_step_bytes and B:
+        out["traffic_per_step"] = pmc_step_bytes
+        out["traffic_over_alg"] = round(pmc_step_bytes / (alg_bytes_trial * B), 3)
+        out["traffic_gbs"] = round(pmc_step_bytes * trials_per_s / B / 1e9, 1)
+    return out
+
+
+def pmc_step_bytes(pmc, names):
+    """Sum of the committed rocprofv3 PMC bytes per launch over one step's pass kernels (measured at
+    cfg2 B = 4096 / cfg5 B = 1024), or None if any is missing."""
+    tot = 0
+    for k in names:
+        v = pmc.get(k, {}).get("hbm_bytes_per_launch")
+        if v is None:
+            return None
+        tot += v
+    return tot
 
 
 def timed_steps(trainer, xs, ys, steps, alg, B, barrier, prof=True):
@@ -134,7 +192,9 @@ def timed_steps(trainer, xs, ys, steps, alg, B, barrier, prof=True):
     return dt, table, dom, kern.get(dom) if dom else None
 
 
-def kernel_table(table, alg, B):
+def kernel_table(table, alg, B, alg_bytes=None):
+    """Per-kernel survey: implemented FLOP rate, implemented bytes rate (x + the planes the kernel
+    reads / writes) and the 8(d) algorithmic bytes rate (x reads only)."""
     out = {}
     tot_all = max(sum(v[1] for v in table.values()), 1e-12)
     for name, (cnt, tot) in table.items():
@@ -142,8 +202,10 @@ def kernel_table(table, alg, B):
         e = {"launches": cnt, "avg_us": round(1e3 * avg_ms, 2), "share": round(tot / tot_all, 4)}
         if name in alg:
             fl, by = alg[name]
-            e["alg_tflops"] = round(fl * B / (avg_ms * 1e-3) / 1e12, 2)
-            e["alg_gbs"] = round(by * B / (avg_ms * 1e-3) / 1e9, 1)
+            e["impl_tflops"] = round(fl * B / (avg_ms * 1e-3) / 1e12, 2)
+            e["impl_gbs"] = round(by * B / (avg_ms * 1e-3) / 1e9, 1)
+            if alg_bytes is not None:
+                e["alg_gbs"] = round(alg_bytes.get(name, 0) * B / (avg_ms * 1e-3) / 1e9, 1)
         out[name] = e
     return out
 
@@ -164,12 +226,13 @@ def bench_train_cfg5(dev, B, steps, warmup, p=0.5):
         tr.step(xs[i % 3], ys[i % 3])
     alg = kernel_algorithmic_wide(C, T, F1, D)
     dt, table, dom, dk = timed_steps(tr, xs, ys, steps, alg, B, lambda: None)
+    ab = kernel_alg_bytes(C, T, wide=True)
+    pmc = load_pmc() if B == 1024 else {}
     roof = None
     if dom and dk:
         fl, by = alg[dom]
-        pmc = load_pmc()
-        roof = roofline_entry(dom, fl * B, by * B, dk[1] / dk[0] * 1e-3,
-                              pmc.get(dom, {}).get("hbm_bytes_per_launch") if B == 1024 else None)
+        roof = roofline_entry(dom, fl * B, ab[dom] * B, by * B, dk[1] / dk[0] * 1e-3,
+                              pmc.get(dom, {}).get("hbm_bytes_per_launch"))
     fl_step = sum(v[0] for v in alg.values())
     tps = B * steps / dt
     return {"metric": "train trials/sec (fwd+CE+bwd+Adam) EEGNet-16,4 64ch x 512, fp32",
@@ -178,7 +241,10 @@ def bench_train_cfg5(dev, B, steps, warmup, p=0.5):
             "implemented_flop_per_trial": fl_step,
             "step_fp32_frac": round(fl_step * tps / (PEAK_FP32_TFLOPS * 1e12), 4),
             "hbm_fraction": round(2 * C * T * 4 * tps / (PEAK_HBM_GBS * 1e9), 4),
-            "roofline": roof, "kernels": kernel_table(table, alg, B)}
+            "roofline": roof,
+            "step_roofline": step_roofline(fl_step, 2 * C * T * 4, sum(v[1] for v in alg.values()), tps,
+                                           pmc_step_bytes(pmc, list(alg) + ["k_coltail"] * 3), B),
+            "kernels": kernel_table(table, alg, B, ab)}
 
 
 def load_pmc():
@@ -200,24 +266,71 @@ def cpu_model_name():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(B, C, T, steps, threads):
-    """Reference CPU path (stock ATen via oracle/torch_ref.py) on this host; trials/s."""
+def cpu_baseline(B, C, T, steps, threads, real_loop=False):
+    """Reference CPU path (stock ATen via oracle/torch_ref.py) on this host; trials/s.
+    ``real_loop``: the reference's own loop body (model.py:136-148) -- float64 batch from the
+    loader, ``signals.float()``, forward, CE, ``loss.item()`` (a sync per step), zero_grad,
+    backward, Adam step."""
     from oracle import torch_ref as tr
     from eegnetreplication_amd import EEGNet
+    prev = torch.get_num_threads()
     torch.set_num_threads(threads)
-    torch.manual_seed(0)
-    state = {k: v.numpy() for k, v in EEGNet(C, T, p=0.5).state_dict().items()}
-    ref = tr.TorchRefEEGNet(state, p=0.5)
-    opt = tr.make_optimizer(ref)
-    rng = np.random.default_rng(1234)
-    x = torch.from_numpy(rng.standard_normal((B, C, T), dtype=np.float32))
-    y = torch.from_numpy(np.random.default_rng(1235).integers(0, 4, B))
-    tr.train_step(ref, opt, x, y)            # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.train_step(ref, opt, x, y)
-    dt = time.perf_counter() - t0
+    try:
+        torch.manual_seed(0)
+        state = {k: v.numpy() for k, v in EEGNet(C, T, p=0.5).state_dict().items()}
+        ref = tr.TorchRefEEGNet(state, p=0.5)
+        opt = tr.make_optimizer(ref)
+        rng = np.random.default_rng(1234)
+        x = rng.standard_normal((B, C, T))
+        x = torch.from_numpy(x) if real_loop else torch.from_numpy(x.astype(np.float32))
+        y = torch.from_numpy(np.random.default_rng(1235).integers(0, 4, B))
+
+        def one():
+            loss, _ = tr.train_step(ref, opt, x.float() if real_loop else x, y)
+            if real_loop:
+                loss.item()
+
+        one()                                    # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
     return B * steps / dt, dt
+
+
+def cpu_baselines(C, T, B, steps):
+    """The cfg2 step at B (best of 1 and 16 threads: the box's CPU share for one GPU is 16; the
+    B = 4096 step's 738 MB intermediates make it memory-bound, so threads help little) and the
+    reference's real loop at batch 64, 22 x 257 (train.py:25,87; model.py:136-148), best of 1 and
+    16 threads.  Returns (cpu_baseline dict, real-loop dict)."""
+    affinity = len(os.sched_getaffinity(0))
+    many = min(16, affinity)
+    legs = {}
+    for th, st in ((many, steps), (1, 2)):
+        v, secs = cpu_baseline(B, C, T, st, th)
+        legs[th] = {"value": round(v, 1), "cores": th, "seconds": round(secs, 2), "steps": st}
+    best = max(legs.values(), key=lambda e: e["value"])
+    cpu = {"value": best["value"], "unit": "trials/s", "cores": best["cores"], "kind": "port",
+           "sample": f"train steps (fwd+CE+bwd+Adam) of B={B} x {C}x{T} after 1 warm-up: best of "
+                     f"{many} threads ({legs[many]['steps']} steps, {legs[many]['seconds']} s) and 1 thread "
+                     f"({legs[1]['steps']} steps, {legs[1]['seconds']} s); {affinity} CPUs in the affinity "
+                     f"mask, {many} = the box's share per GPU; torch {torch.__version__} CPU, "
+                     f"{cpu_model_name()}",
+           "legs": list(legs.values())}
+    real = {}
+    for th in (many, 1):
+        v, secs = cpu_baseline(64, 22, 257, 40, th, real_loop=True)
+        real[th] = {"value": round(v, 1), "cores": th, "seconds": round(secs, 2)}
+    rb = max(real.values(), key=lambda e: e["value"])
+    real_out = {"value": rb["value"], "unit": "trials/s", "cores": rb["cores"], "kind": "port",
+                "sample": "40 steps of the reference loop body (float64 batch -> .float(), forward, CE, "
+                          ".item(), zero_grad, backward, Adam) at batch 64 x 22x257 after 1 warm-up, "
+                          f"best of {many} threads and 1 thread",
+                "legs": list(real.values())}
+    cpu["real_protocol_b64_t257"] = real_out
+    return cpu, real_out
 
 
 INFER_BF16_BYTES = lambda C, T: 2 * C * T + 16          # bf16 x in, fp32 logits out, per trial
@@ -310,6 +423,51 @@ def bench_folds(dev, n_folds, n_train, epochs):
             "sequential_folds_value": round(alone, 1), "speedup": round(fused / alone, 2)}
 
 
+def bench_cfg4(dev, rank, world, G, steps, warmup, barrier, nx=2):
+    """BASELINE configs[3]: EEGNet-8,2 data parallel at global batch G = 65,536 split over the
+    ranks (strong scaling: G / world trials per rank per step), one all-reduce per step
+    (DataParallelTrainer; the fused single-device step at world 1).  Runs on every rank; returns
+    the rank-0 record (None elsewhere)."""
+    from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
+    from eegnetreplication_amd.distributed import DataParallelTrainer
+    C, T = 22, 256
+    B = G // world
+    torch.manual_seed(0)
+    model = EEGNet(C, T, F1=8, D=2, p=0.5).to(dev).train()
+    g = torch.Generator(device=dev).manual_seed(4242 + rank)
+    xs = [torch.randn(B, C, T, device=dev, generator=g) for _ in range(nx)]
+    ys = [torch.randint(0, 4, (B,), device=dev, generator=g) for _ in range(nx)]
+    tr = DataParallelTrainer(model) if world > 1 else FusedTrainer(model)
+    for i in range(warmup):
+        tr.step(xs[i % nx], ys[i % nx])
+    alg = kernel_algorithmic(C, T)
+    dt, table, dom, dk = timed_steps(tr, xs, ys, steps, alg, B, barrier)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    del xs, ys
+    if rank != 0:
+        return None
+    tps = G * steps / dt
+    ab = kernel_alg_bytes(C, T)
+    roof = None
+    if dom and dk:
+        fl, by = alg[dom]
+        roof = roofline_entry(dom, fl * B, ab[dom] * B, by * B, dk[1] / dk[0] * 1e-3, None)
+    flop = sum(v[0] for v in alg.values())
+    return {"metric": "train trials/sec (fwd+CE+bwd+Adam) EEGNet-8,2 22ch x 256, data parallel",
+            "value": round(tps, 1), "unit": "trials/s", "global_batch": G, "batch_per_gpu": B,
+            "n_gpus": world, "steps": steps, "warmup": warmup, "scaling": "strong",
+            "ms_per_step": round(1e3 * dt / steps, 4), "loss": round(float(tr.loss.item()), 5),
+            "collectives_per_step": 1 if world > 1 else 0,
+            "roofline": roof,
+            "step_roofline": step_roofline(flop, ALG_BYTES_PER_TRIAL, sum(v[1] for v in alg.values()),
+                                           tps / world),
+            "hbm_fraction": round(ALG_BYTES_PER_TRIAL * tps / (PEAK_HBM_GBS * 1e9 * world), 4),
+            "kernels": kernel_table(table, alg, B, ab)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -330,6 +488,9 @@ def main():
     ap.add_argument("--nx", type=int, default=4, help="distinct x buffers rotated in the timed region")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 EEGNet-16,4 training leg")
     ap.add_argument("--cfg5-batch", type=int, default=1024)
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 global-batch-65536 leg")
+    ap.add_argument("--global-batch", type=int, default=CFG4_GLOBAL_BATCH,
+                    help="cfg4 leg: global batch split over the ranks (strong scaling)")
     args = ap.parse_args()
 
     from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
@@ -371,14 +532,19 @@ def main():
     ms_per_step = 1e3 * dt / args.steps
     trials_per_s = world * B * args.steps / dt
 
+    del xs, ys
+    cfg4 = None
+    if not args.no_cfg4:
+        cfg4 = bench_cfg4(dev, rank, world, args.global_batch, steps=10, warmup=3, barrier=barrier)
     if rank == 0:
-        per_kernel = kernel_table(table, alg, B)
+        ab = kernel_alg_bytes(C, T)
+        per_kernel = kernel_table(table, alg, B, ab)
+        pmc = load_pmc() if (B, C, T) == (4096, 22, 256) else {}
         roof = None
         if dom is not None and dk:
             fl, by = alg[dom]
-            pmc = load_pmc()
-            roof = roofline_entry(dom, fl * B, by * B, dk[1] / dk[0] * 1e-3,
-                                  pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc else None)
+            roof = roofline_entry(dom, fl * B, ab[dom] * B, by * B, dk[1] / dk[0] * 1e-3,
+                                  pmc.get(dom, {}).get("hbm_bytes_per_launch"))
         impl_flop = sum(v[0] for v in alg.values())
         impl_bytes = sum(v[1] for v in alg.values())
         infer = None
@@ -389,19 +555,9 @@ def main():
             folds = bench_folds(dev, args.folds, 1440, epochs=2)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            # the box's CPU share for one GPU is 16 cores (OMP_NUM_THREADS=16 there); all of them,
-            # then one thread on a smaller batch of the same step
-            affinity = len(os.sched_getaffinity(0))
-            threads = min(16, affinity)
-            v, secs = cpu_baseline(B, C, T, args.cpu_steps, threads)
-            v1, secs1 = cpu_baseline(512, C, T, 2, 1)
-            cpu = {"value": round(v, 1), "unit": "trials/s", "cores": threads, "kind": "port",
-                   "sample": f"{args.cpu_steps} train steps (fwd+CE+bwd+Adam) of B={B} x {C}x{T} "
-                             f"after 1 warm-up, {secs:.1f} s, {threads} threads (the box's CPU share; "
-                             f"{affinity} in the affinity mask), torch {torch.__version__} CPU, "
-                             f"{cpu_model_name()}",
-                   "one_thread": {"value": round(v1, 1), "unit": "trials/s", "cores": 1,
-                                  "sample": f"2 steps of B=512 x {C}x{T} after 1 warm-up, {secs1:.1f} s"}}
+            cpu, real_cpu = cpu_baselines(C, T, B, args.cpu_steps)
+            if folds is not None:
+                folds["cpu_baseline"] = real_cpu
         cfg5 = None
         if not args.no_cfg5:
             cfg5 = bench_train_cfg5(dev, args.cfg5_batch, steps=10, warmup=3)
@@ -423,17 +579,20 @@ def main():
                        "model": "EEGNet-8,2", "global_batch": B * world, "seq_len": T,
                        "channels": C, "parallelism": f"dp{world}"},
             "roofline": roof,
+            "step_roofline": step_roofline(impl_flop, ALG_BYTES_PER_TRIAL, impl_bytes, trials_per_s / world,
+                                           pmc_step_bytes(pmc, alg), B),
             "cpu_baseline": cpu,
-            "hbm_fraction": round(ALG_BYTES_PER_TRIAL * trials_per_s / (PEAK_HBM_GBS * 1e9), 4),
-            "step_fp32_frac": round(impl_flop * trials_per_s / (PEAK_FP32_TFLOPS * 1e12), 4),
+            "hbm_fraction": round(ALG_BYTES_PER_TRIAL * trials_per_s / world / (PEAK_HBM_GBS * 1e9), 4),
+            "step_fp32_frac": round(impl_flop * trials_per_s / world / (PEAK_FP32_TFLOPS * 1e12), 4),
             "implemented_flop_per_trial": impl_flop,
             # the step's own HBM traffic (x twice, the s / v planes, the block-2 planes) against peak
             "implemented_bytes_per_trial": impl_bytes,
-            "step_hbm_frac": round(impl_bytes * trials_per_s / (PEAK_HBM_GBS * 1e9), 4),
+            "step_hbm_frac": round(impl_bytes * trials_per_s / world / (PEAK_HBM_GBS * 1e9), 4),
             "x_buffers": args.nx,
             "ref_formulation_tflops": round(REF_FLOP_PER_TRIAL * trials_per_s / 1e12, 2),
             "kernels": per_kernel,
             "final_loss": round(loss, 5),
+            "cfg4_dp": cfg4,
             "cfg5_train": cfg5,
             "cfg5_infer_bf16": infer,
             "real_protocol_folds": folds,

@@ -290,8 +290,9 @@ static void set_attrs_shape() {
                           (const void*)k_pass_c<K1, CC, TT, FF>, (const void*)k_pass_d<K1, CC, TT, FF>,
                           (const void*)k_pass_e<K1, CC, TT, FF>, (const void*)k_pass_a<K1, CC, TT, FF, true>,
                           (const void*)k_pass_b<K1, CC, TT, FF, true>, (const void*)k_pass_c<K1, CC, TT, FF, true>,
-                          (const void*)k_pass_d<K1, CC, TT, FF, true>, (const void*)k_pass_e<K1, CC, TT, FF, true>,
-                          (const void*)k_pass_d<K1, CC, TT, FF, false, false>})
+                          (const void*)k_pass_e<K1, CC, TT, FF, true>,
+                          (const void*)k_pass_d<K1, CC, TT, FF, false, false>,
+                          (const void*)k_pass_d<K1, CC, TT, FF, true, false>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipFuncSetAttribute((const void*)k_infer<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
@@ -484,7 +485,7 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     } else {
     { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
     } LAUNCH_CHECK("k_pass_c(bwd)");
-#define LAUNCH_D(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, true>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
+#define LAUNCH_D(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, true, false>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
                        m2, m3, dl, (float*)(ws + L.dp2), \
@@ -767,6 +768,26 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
         : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, ap, s);
 }
 
+}  // extern "C"
+
+// trials per workgroup of the fold-indexed launches: streaming passes A / B / E, passes C / D, the
+// whole-trial block-2 passes (EEGNET_B2=1).  The defaults reproduce the 90-fold real-protocol grids
+// of a batch of 64 (5 / 2 / 11 workgroups per fold); EEGNET_FOLD_TPW="s,c,b2" overrides them (sweeps).
+static void fold_tpw(int* s, int* c, int* b2) {
+    static int v[3] = {0, 0, 0};
+    if (v[0] == 0) {
+        int a = 13, b = 32, d = 6;
+        if (const char* e = getenv("EEGNET_FOLD_TPW")) {
+            int x = 0, y = 0, z = 0;
+            if (sscanf(e, "%d,%d,%d", &x, &y, &z) == 3 && x > 0 && y > 0 && z > 0) { a = x; b = y; d = z; }
+        }
+        v[1] = b; v[2] = d; v[0] = a;
+    }
+    *s = v[0]; *c = v[1]; *b2 = v[2];
+}
+
+extern "C" {
+
 int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fold* folds, int64_t row0,
                             int64_t slot, uint64_t offset, float lr, float beta1, float beta2, float eps,
                             void* stream) {
@@ -780,13 +801,16 @@ int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fo
     set_key(&g, 0, offset);                           // the keep threshold (keys come per fold)
     ensure_attrs();
     const WsLayout L = make_layout(g);
-    // the folds share the chip: per fold, the workgroups of a full-chip grid divided by nfolds, so
-    // each workgroup runs several trials (its prologue and the reduction tail are per workgroup)
-    // and all folds are resident at once.  Fewer partial rows than the workspace holds: fine.
-    const int cus = device_cus();
-    g.gridS = std::max(1, std::min(g.B, WGPC * cus / nfolds));
-    g.grid = std::max(1, std::min(g.B, cus / nfolds));
-    g.gridB2 = std::max(1, std::min(g.B, 4 * cus / nfolds));
+    // the folds share the chip: each workgroup runs several trials of its fold (its prologue and the
+    // reduction tail are per workgroup).  The per-fold grid is a function of B alone -- never of
+    // nfolds -- so a fold's trial -> workgroup split, and with it every partial sum and every bit of
+    // its result, does not depend on how many folds share the launch (fold-batch width, sharding
+    // over ranks).  Capped at the non-fold grids the workspace's partial rows are sized for.
+    int tpwS, tpwC, tpwB2;
+    fold_tpw(&tpwS, &tpwC, &tpwB2);
+    g.gridS = std::max(1, std::min(g.gridS, (g.B + tpwS - 1) / tpwS));
+    g.grid = std::max(1, std::min(g.grid, (g.B + tpwC - 1) / tpwC));
+    g.gridB2 = std::max(1, std::min(g.gridB2, (g.B + tpwB2 - 1) / tpwB2));
     FoldCall fc;
     memset(&fc, 0, sizeof(fc));
     fc.folds = folds;

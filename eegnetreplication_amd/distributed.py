@@ -6,9 +6,9 @@ Two shapes of parallelism, one process per GPU (torch.distributed; backend "nccl
   the flat fp32 gradient (1,716 floats = 6.9 KB for EEGNet-8,2) is summed with ONE all-reduce per
   step, averaged, then clamped (model.py:44/84 hooks AFTER the reduction, so the clamp sees the
   global-batch gradient) and Adam runs replicated.  BatchNorm normalises with per-rank
-  batch statistics and broadcasts rank 0's running statistics each step (DDP's defaults).  The
-  gradient message is latency-bound (~7 KB), so there is exactly one gradient collective per step
-  and nothing to bucket.
+  batch statistics; rank 0's running statistics and the global mean loss ride in the same message
+  (DDP's broadcast_buffers).  The message is latency-bound (~7 KB), so there is exactly one
+  collective per step and nothing to bucket.
 * fold sharding (cfg3): independent cross-/within-subject folds are dealt to ranks by
   longest-processing-time order with no communication on the data path; results are merged on the
   host (``gather_results``).
@@ -54,13 +54,22 @@ def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
 
 
 class DataParallelTrainer:
-    """Fused HIP train step + one RCCL gradient all-reduce per step (cfg4).
+    """Fused HIP train step + ONE collective per step (cfg4).
 
-    Per step (``step``): [buffer broadcast] -> local gradients (HIP, clamps deferred) -> all-reduce
-    mean -> model.py:44/84 clamps -> Adam, replicated on every rank.  BatchNorm normalises with
-    per-rank batch statistics; the running statistics follow DDP's default
-    ``broadcast_buffers=True``: rank 0's running_mean/var and num_batches_tracked are broadcast to
-    every rank before each local forward, so every rank evaluates and checkpoints rank 0's buffers.
+    Per step (``step``): local gradients (HIP, clamps deferred) -> one all-reduce (SUM) of the flat
+    communication buffer ``[grads | loss | BN running statistics]`` -> x 1/world on the gradient and
+    the loss -> model.py:44/84 clamps -> Adam, replicated on every rank.
+
+    BatchNorm normalises with per-rank batch statistics.  Running statistics follow DDP's default
+    ``broadcast_buffers=True`` -- every rank ends each step holding rank 0's -- but they travel in the
+    same all-reduce as the gradient: rank 0 contributes its freshly updated buffers, every other rank
+    contributes zeros, so the sum IS rank 0's buffers (x + 0 == x exactly).  In train mode the
+    forward reads batch statistics, never the running ones, so moving the broadcast from before the
+    forward (DDP) to after it changes no result; it leaves every rank with rank 0's buffers after
+    every step, including the last (what eval and checkpoints read).  ``num_batches_tracked`` is
+    broadcast once at construction with the parameters: every rank then adds exactly one per step.
+    The loss returned is the global-batch mean (the all-reduced per-rank means / world).
+
     The stages are methods so the orchestration can be exercised on CPU (gloo) with stand-ins for
     the device kernels.
     """
@@ -74,8 +83,8 @@ class DataParallelTrainer:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         flat = model.flat_parameters()
-        if self.world > 1:   # identical start on every rank
-            dist.broadcast(flat, self._src(0), group=group)
+        if self.world > 1:   # identical start on every rank: parameters, BN buffers and counters
+            self.broadcast_state()
         self._init_state(flat)
         self._ws = {}
         self._step = 0
@@ -84,8 +93,25 @@ class DataParallelTrainer:
         return dist.get_global_rank(self.group, r) if self.group is not None else r
 
     def _init_state(self, flat):
+        n, nb = flat.numel(), self.model.flat_bn_buffers().numel()
         self.adam = FusedAdamState(self.model)
-        self.loss = torch.zeros(1, dtype=torch.float32, device=flat.device)
+        # the step's single message: [grads n | loss 1 | BN running statistics nb], fp32
+        self.comm = torch.zeros(n + 1 + nb, dtype=torch.float32, device=flat.device)
+        self.adam.grads = self.comm[:n]
+        self.loss = self.comm[n:n + 1]
+
+    def broadcast_state(self):
+        """Rank 0's parameters, BN running statistics and num_batches_tracked to every rank, as ONE
+        float64 broadcast (fp32 and the int64 counters below 2^53 round-trip exactly)."""
+        m = self.model
+        flat, bn, nbt = m.flat_parameters(), m.flat_bn_buffers(), m.flat_num_batches_tracked()
+        buf = torch.cat([flat.detach().double(), bn.double(), nbt.double()])
+        dist.broadcast(buf, self._src(0), group=self.group)
+        n, nb = flat.numel(), bn.numel()
+        with torch.no_grad():
+            flat.copy_(buf[:n])
+            bn.copy_(buf[n:n + nb])
+            nbt.copy_(buf[n + nb:].round().to(torch.int64))
 
     def workspace(self, B):
         ws = self._ws.get(B)
@@ -95,12 +121,6 @@ class DataParallelTrainer:
         return ws
 
     # -- stages ------------------------------------------------------------------------------
-    def sync_buffers(self):
-        """DDP broadcast_buffers: rank 0's BN running statistics and counters to every rank."""
-        if self.world > 1:
-            dist.broadcast(self.model.flat_bn_buffers(), self._src(0), group=self.group)
-            dist.broadcast(self.model.flat_num_batches_tracked(), self._src(0), group=self.group)
-
     def local_grads(self, x, y, seed, offset):
         m = self.model
         ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
@@ -109,8 +129,25 @@ class DataParallelTrainer:
         return self.adam.grads
 
     def reduce(self, grads):
-        """ONE all-reduce (SUM) of the flat gradient, then x 1/world: CE is a batch mean."""
-        return allreduce_mean_(grads, self.group)
+        """ONE all-reduce (SUM) of [grads | loss | rank 0's BN buffers], then x 1/world on the
+        gradient and the loss (CE is a batch mean) and rank 0's buffers into every rank's BN."""
+        if self.world == 1:
+            return grads
+        n = grads.numel()
+        bn = self.model.flat_bn_buffers()
+        tail = self.comm[n + 1:]
+        if not self.broadcast_buffers:
+            tail.zero_()
+        elif self.rank == 0:
+            tail.copy_(bn)
+        else:
+            tail.zero_()
+        dist.all_reduce(self.comm, op=dist.ReduceOp.SUM, group=self.group)
+        self.comm[:n + 1].mul_(1.0 / self.world)
+        if self.broadcast_buffers:
+            with torch.no_grad():
+                bn.copy_(tail)
+        return grads
 
     def clamp(self, grads):
         ops.clamp_grads(self.model.shape, grads)
@@ -125,8 +162,6 @@ class DataParallelTrainer:
         self._step += 1
         seed = 0x5EED_0000 + self._step
         offset = self._step * self.world + self.rank        # distinct masks on every rank
-        if self.broadcast_buffers:
-            self.sync_buffers()
         grads = self.local_grads(x, y, seed, offset)
         self.reduce(grads)
         self.clamp(grads)

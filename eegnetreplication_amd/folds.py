@@ -9,11 +9,12 @@ parameters, BN buffers, Adam state and workspace each) and enqueues step j of ev
 step j+1 of any, each fold on its own HIP stream, so the kernels of different folds overlap on
 the device and no host synchronisation happens inside an epoch.
 
-Per fold the arithmetic is exactly ``FusedTrainer.step`` (model.py:141-148 semantics: forward,
-CE, backward with the two clamps, Adam); only the interleaving changes.  Dropout keys are
-counter-based per fold -- (fold seed, step counter) -- so a fold's trajectory does not depend on
-how many other folds run beside it (tests/test_gpu_folds.py checks bit-equality with the same fold
-run alone).
+Per fold the arithmetic is ``FusedTrainer.step``'s (model.py:141-148 semantics: forward, CE,
+backward with the two clamps, Adam); only the interleaving changes.  Dropout keys are
+counter-based per fold -- (fold seed, step counter) -- and a fold-indexed launch splits each fold's
+batch over workgroups by the batch size alone, so a fold's trajectory does not depend on how many
+other folds run beside it or on which rank it was dealt to (tests/test_gpu_folds.py checks
+bit-equality with the same fold run alone).
 """
 
 from __future__ import annotations
@@ -90,17 +91,31 @@ class FoldBatch:
                            nbt=m.flat_num_batches_tracked(), key_from_step=True)
 
     # -- fused launches: all folds in one grid --------------------------------------------------
+    def _fused_key(self, data, batch_size):
+        """Everything a fold table or the captured graph holds a raw device pointer to: each
+        model's flat parameters, BN buffers, counters, Adam state and gradients, and the identity
+        of every fold's X and y.  ``.to()`` / ``.cuda()`` / ``.float()`` or a re-flatten re-creates
+        the model buffers; a caller may pass new y tensors with the same X."""
+        ptrs = []
+        for m, a in zip(self.models, self.adam):
+            ptrs += [m.flat_parameters().data_ptr(), m.flat_bn_buffers().data_ptr(),
+                     m.flat_num_batches_tracked().data_ptr(), a.state.data_ptr(), a.grads.data_ptr(),
+                     a.step.data_ptr()]
+        return (data[0][0].shape[0], batch_size, tuple(ptrs),
+                tuple((id(X), X.data_ptr(), id(y), y.data_ptr()) for X, y in data))
+
     def _fused_state(self, data, batch_size):
         X0, _ = data[0]
         n = X0.shape[0]
+        key = self._fused_key(data, batch_size)
         st = self._fz
-        if st is not None and st["n"] == n and st["bs"] == batch_size and \
-                all(a is d[0] for a, d in zip(st["src"], data)):
+        if st is not None and st["key"] == key:
             return st
         dev = X0.device
         K = len(self.models)
         nsteps = (n + batch_size - 1) // batch_size
-        st = {"n": n, "bs": batch_size, "src": [d[0] for d in data], "graph": None,
+        # any change: new tables, and the graph (which baked the old pointers in) is dropped
+        st = {"key": key, "src": [d for d in data], "graph": None,
               "Xp": [torch.empty_like(X) for X, _ in data], "yp": [torch.empty_like(y) for _, y in data],
               "perm": [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(K)],
               "losses": [torch.zeros(nsteps, dtype=torch.float32, device=dev) for _ in range(K)],

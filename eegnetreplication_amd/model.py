@@ -65,7 +65,12 @@ class EEGNet(nn.Module):
         """Re-home every parameter (and BN running stat) as a view of one flat fp32 buffer, in
         named_parameters() order -- the layout of include/eegnet_abi.h.  Parameter identity is
         kept (``.data`` is rebound), so optimizers built before ``.to()`` keep working."""
-        params = list(self.parameters())
+        # (module, attribute) of every parameter, in named_parameters() order: _flat_ok checks that
+        # each slot still holds the Parameter re-homed here (a caller may assign a new one)
+        self._pslots = [(mod, name) for mod in self.modules() for name, q in mod._parameters.items()
+                        if q is not None]
+        params = [mod._parameters[name] for mod, name in self._pslots]
+        assert len(params) == len(list(self.parameters()))
         dev = params[0].device
         n = sum(p.numel() for p in params)
         flat = torch.empty(n, dtype=torch.float32, device=dev)
@@ -115,7 +120,10 @@ class EEGNet(nn.Module):
 
     def _flat_ok(self) -> bool:
         """Every parameter / BN buffer still a view of the flat buffers (a caller may rebind
-        ``p.data`` or a buffer)."""
+        ``p.data``, assign a new Parameter or replace a buffer)."""
+        for (mod, name), p in zip(self._pslots, self._plist):
+            if mod._parameters.get(name) is not p:
+                return False
         bns = self._bns()
         for i, bn in enumerate(bns):
             if bn.running_mean is not self._blist[2 * i] or bn.running_var is not self._blist[2 * i + 1] \

@@ -17,7 +17,9 @@ Same protocols, hyper-parameters, checkpoint names and JSON report schema as the
 MI355X specifics: the folds are independent units, dealt to ranks (one process per GPU) by
 ``distributed.lpt_assign`` with no communication on the data path and merged on the host; every
 split lives in HBM (``DeviceLoader``); each unit is seeded (``--seed`` + unit index), which the
-reference does not do, so results do not depend on how units are sharded.
+reference does not do, and a fold-indexed launch splits a fold's batch over workgroups by
+the batch size alone, so results do not depend on how units are sharded or batched
+(tests/test_gpu_sharding.py).  A unit that fails on the host is re-run once from a fresh state.
 """
 
 from __future__ import annotations
@@ -120,17 +122,47 @@ def _run_folds(specs, epochs, device):
     return out
 
 
+UNIT_RETRIES = 1
+
+
+def _device_fault(e: BaseException) -> bool:
+    """A failure of the device itself (HIP error, fault): the context is unusable, so the unit is
+    not retried -- the process exits non-zero and the driver re-runs it."""
+    msg = str(e)
+    return isinstance(e, getattr(torch, "AcceleratorError", ())) or "HIP error" in msg or "CUDA error" in msg
+
+
+def _with_retry(fn, what, retries=None):
+    """Run one idempotent unit (a fold, or a batch of folds), re-running it from a fresh state if a
+    host-side exception escapes (a fold is an idempotent unit).  Every unit builds its
+    model, generator and loaders from its own seed, so a re-run reproduces the result bit for bit."""
+    retries = UNIT_RETRIES if retries is None else retries
+    for attempt in range(retries + 1):
+        try:
+            return fn()
+        except Exception as e:                       # noqa: BLE001 -- re-raised below
+            if attempt == retries or _device_fault(e):
+                raise
+            logger.warning(f"{what} failed ({e!r}); re-running it from a fresh state "
+                           f"(attempt {attempt + 2}/{retries + 1})")
+    raise AssertionError("unreachable")
+
+
 def _run_units(specs, epochs, device, fold_batch):
-    """Run unit specs one by one (_run_fold) or fold_batch at a time (_run_folds)."""
+    """Run unit specs one by one (_run_fold) or fold_batch at a time (_run_folds), each unit (or
+    fold batch) retried once from a fresh state on a host-side failure."""
     if fold_batch <= 1:
-        return [_run_fold(*sp[:5], sp[5], epochs, sp[6], device) for sp in specs]
+        return [_with_retry(lambda sp=sp: _run_fold(*sp[:5], sp[5], epochs, sp[6], device), f"unit {i}")
+                for i, sp in enumerate(specs)]
     # balanced batches of at most fold_batch units (90 cross-subject folds at 48: 45 + 45, not 48 + 42):
     # one fold-indexed launch per pass serves a whole batch, so its size sets the launch width
     nb = -(-len(specs) // fold_batch)
     size = -(-len(specs) // nb) if nb else 0
     res = []
     for i in range(0, len(specs), max(size, 1)):
-        res.extend(_run_folds(specs[i:i + size], epochs, device))
+        batch = specs[i:i + size]
+        res.extend(_with_retry(lambda b=batch: _run_folds(b, epochs, device),
+                               f"fold batch of units {i}..{i + len(batch) - 1}"))
     return res
 
 

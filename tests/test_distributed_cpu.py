@@ -1,6 +1,6 @@
 """Multi-process orchestration on CPU (gloo, world_size 2): the product DataParallelTrainer.step
-(buffer broadcast -> local step -> all-reduce mean -> clamp -> Adam), and fold sharding / result
-gathering.  The device stages are stand-ins here (the local step is the float64 oracle); their HIP
+(local step -> ONE all-reduce of [grads | loss | rank 0's BN buffers] -> mean -> clamp -> Adam), and
+fold sharding / result gathering.  The device stages are stand-ins here (the local step is the float64 oracle); their HIP
 kernels are checked on the GPU in tests/test_gpu_distributed.py."""
 
 from __future__ import annotations
@@ -49,10 +49,11 @@ def _rank_grads(rank, world):
 
 
 def _worker(rank, world, port, q):
-    """Drives the product DataParallelTrainer.step (buffer broadcast -> local grads -> reduce ->
-    clamp -> update) on CPU/gloo.  Only the device stages are stand-ins: local_grads returns the
-    oracle's unclamped local gradient, clamp / update record what reaches them (the HIP clamp and
-    Adam kernels are checked on the GPU: tests/test_gpu_distributed.py)."""
+    """Drives the product DataParallelTrainer.step (local grads -> reduce -> clamp -> update) on
+    CPU/gloo.  Only the device stages are stand-ins: local_grads writes the oracle's unclamped local
+    gradient, a rank-specific loss and a rank-specific running-statistics update (what the HIP
+    forward does to the BN buffers); clamp / update record what reaches them (the HIP clamp and Adam
+    kernels are checked on the GPU: tests/test_gpu_distributed.py)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from eegnetreplication_amd import EEGNet
@@ -68,7 +69,11 @@ def _worker(rank, world, port, q):
 
     def local_grads(x, y, seed, offset):
         calls.append(("local", seed, offset, model.flat_bn_buffers().clone()))
-        tr.adam.grads = _rank_grads(rank, world).float()
+        tr.adam.grads.copy_(_rank_grads(rank, world).float())
+        tr.loss.fill_(1.0 + rank)                               # per-rank batch-mean loss
+        with torch.no_grad():                                   # the forward's running-stat update
+            model.flat_bn_buffers().mul_(0.9).add_(0.1 * (rank + 3))
+            model.flat_num_batches_tracked().add_(1)
         return tr.adam.grads
 
     def clamp(grads):
@@ -86,7 +91,7 @@ def _worker(rank, world, port, q):
     merged = D.gather_results(local)
     q.put((rank, [c[0] for c in calls], calls[0][1:3], calls[0][3].numpy(), calls[1][1].numpy(),
            calls[2][1], model.flat_parameters().detach().numpy().copy(), nbt.numpy(),
-           sorted(merged.items()), assign))
+           sorted(merged.items()), assign, model.flat_bn_buffers().numpy().copy(), float(tr.loss)))
     dist.destroy_process_group()
 
 
@@ -106,8 +111,12 @@ def test_dp_trainer_step_order_and_fold_sharding():
     for r in res:
         assert r[1] == ["local", "clamp", "update"]          # clamp after the reduction, then Adam
         assert r[5] is True                                   # Adam consumes the reduced buffer
-        np.testing.assert_array_equal(r[3], np.ones_like(r[3]))  # rank 0's BN buffers broadcast first
-        np.testing.assert_array_equal(r[7], [10, 10, 10])
+        np.testing.assert_array_equal(r[3], np.ones_like(r[3]))  # rank 0's BN buffers at construction
+        np.testing.assert_array_equal(r[7], [11, 11, 11])        # rank 0's counters, + 1 per step
+        # after the step every rank holds rank 0's updated running statistics (DDP broadcast_buffers),
+        # carried by the gradient all-reduce (x + 0 == x), and the global-batch mean loss
+        np.testing.assert_array_equal(r[10], np.full_like(r[10], np.float32(np.float32(0.9) * 1.0 + np.float32(0.3))))
+        assert r[11] == 1.5
     # distinct dropout keys per rank, same seed
     assert res[0][2][0] == res[1][2][0] and res[0][2][1] != res[1][2][1]
     # identical parameters on every rank after the initial broadcast

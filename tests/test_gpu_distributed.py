@@ -156,10 +156,11 @@ def _dp_worker(rank, world, port, q):
         y = torch.from_numpy(g.y[rank * half:(rank + 1) * half]).to(dev)
         tr.step(x, y)
         torch.cuda.synchronize()
-        q.put((rank, model.flat_parameters().cpu().numpy().copy(), float(tr.loss.item()), None))
+        q.put((rank, model.flat_parameters().cpu().numpy().copy(), float(tr.loss.item()), None,
+               model.flat_bn_buffers().cpu().numpy().copy()))
         dist.destroy_process_group()
     except Exception as e:                 # report instead of hanging the parent
-        q.put((rank, None, None, repr(e)))
+        q.put((rank, None, None, repr(e), None))
         raise
 
 
@@ -185,16 +186,20 @@ def test_dp_trainer_world2_on_one_gpu():
     for p in procs:
         assert p.exitcode == 0
     np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_array_equal(res[0][4], res[1][4])      # rank 0's running statistics everywhere
+    assert res[0][2] == res[1][2]                             # the global-batch mean loss
     g = Golden("G6")
     params, bufs = g.init_params(), g.init_buffers()
     half = g.x.shape[0] // world
-    acc = None
+    acc, losses = None, []
     for r in range(world):
         logits, cache, _ = nr.forward(params, bufs, g.x[r * half:(r + 1) * half], train=True, p=0.0)
-        _, dl = nr.cross_entropy(logits, g.y[r * half:(r + 1) * half])
+        lr_, dl = nr.cross_entropy(logits, g.y[r * half:(r + 1) * half])
+        losses.append(float(lr_))
         gr = nr.backward(cache, dl, clamp=False)
         acc = gr if acc is None else {k: acc[k] + gr[k] for k in acc}
     mean = {k: v / world for k, v in acc.items()}
+    assert abs(res[0][2] - sum(losses) / world) <= 1e-4 * max(1.0, abs(sum(losses) / world))
     mean["spatial.weight"] = np.clip(mean["spatial.weight"], -1.0, 1.0)
     mean["classifier.weight"] = np.clip(mean["classifier.weight"], -0.25, 0.25)
     expect = nr.adam_step(params, mean, nr.adam_init(params))

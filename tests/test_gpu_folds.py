@@ -1,9 +1,12 @@
 """Fold-batched training (eegnetreplication_amd.folds.FoldBatch) on the GPU.
 
-FoldBatch only interleaves independent fused steps over HIP streams, so the bar is bit-equality:
-every fold of a concurrent batch must end with exactly the parameters, BN buffers, Adam state and
-loss sums of the same fold trained alone, and a one-fold batch must reproduce FusedTrainer, whose
-step is pinned to the oracle and the reference golden vectors by tests/test_gpu_parity.py.
+FoldBatch only interleaves independent steps (per-fold HIP streams running FusedTrainer's step, or
+fold-indexed launches), so the bar is bit-equality: every fold of a concurrent batch must end with
+exactly the parameters, BN buffers, Adam state and loss sums of the same fold trained alone, and a
+one-fold stream batch must reproduce FusedTrainer, whose step is pinned to the oracle and the
+reference golden vectors by tests/test_gpu_parity.py.  A fold-indexed launch splits a fold's batch
+over fewer workgroups than FusedTrainer (by the batch size alone: eegnet_host.hip fold_tpw), so
+against FusedTrainer it agrees to the fp32 rounding of its partial sums, not bit for bit.
 Shapes follow the real protocol: 22 x 257 trials (02_preprocessing_pipeline.ipynb:1867), batch 64
 with a short last batch (train.py:87, DataLoader drop_last=False).
 """
@@ -17,6 +20,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 C, T = 22, 257
+PARAMS = ("temporal.0.weight", "temporal.1.weight", "temporal.1.bias", "spatial.weight",
+          "aggregation.0.weight", "aggregation.0.bias", "block_2.0.weight", "block_2.1.weight",
+          "block_2.2.weight", "block_2.2.bias", "classifier.weight", "classifier.bias")
 
 
 def _dev():
@@ -66,7 +72,7 @@ def test_concurrent_folds_equal_each_fold_alone():
     sums_all = [fb.epoch(data, 64, gens) for _ in range(2)]
     torch.cuda.synchronize()
     for k in range(3):
-        one = FoldBatch([alone[k]], [seeds[k]])
+        one = FoldBatch([alone[k]], [seeds[k]], fused=False)      # the same per-fold stream path
         g = [torch.Generator().manual_seed(seeds[k])]
         sums_one = [one.epoch([data[k]], 64, g) for _ in range(2)]
         torch.cuda.synchronize()
@@ -78,13 +84,19 @@ def test_concurrent_folds_equal_each_fold_alone():
         assert int(fb.adam[k].step.item()) == 2 * ((sizes[k] + 63) // 64)
 
 
-def test_single_fold_matches_fused_trainer():
+@pytest.mark.parametrize("fused", [False, True])
+def test_single_fold_matches_fused_trainer(fused):
+    """fused=False (one stream per fold): FusedTrainer's launches, bit for bit.  fused=True (a
+    fold-indexed launch, fewer workgroups per fold): the same step to fp32 rounding -- parameters
+    at golden_util's post-Adam tolerance, the BN1 / BN3 running statistics at rtol 1e-4 (BN2's
+    follow gamma1 / beta1, whose gradients are rounding residue: DESIGN 7)."""
+    from golden_util import assert_params_close
     from eegnetreplication_amd import FoldBatch, FusedTrainer
     dev = _dev()
     X, y = _data(150, 5, dev)
     (m,) = _models(1, 0.0, dev)           # p = 0: the dropout key stream does not matter
     ref = _clone(m, 0.0, dev)
-    fb = FoldBatch([m], [1])
+    fb = FoldBatch([m], [1], fused=fused)
     fb.epoch([(X, y)], 64, [torch.Generator().manual_seed(3)])
     from eegnetreplication_amd.dataset import epoch_permutation
     perm = epoch_permutation(150, torch.Generator().manual_seed(3)).to(dev)
@@ -93,9 +105,20 @@ def test_single_fold_matches_fused_trainer():
         idx = perm[i:i + 64]
         tr.step(X.index_select(0, idx), y.index_select(0, idx))
     torch.cuda.synchronize()
-    assert torch.equal(m.flat_parameters(), ref.flat_parameters())
-    assert torch.equal(m.flat_bn_buffers(), ref.flat_bn_buffers())
-    assert torch.equal(fb.adam[0].state, tr.adam.state)
+    if not fused:
+        assert torch.equal(m.flat_parameters(), ref.flat_parameters())
+        assert torch.equal(m.flat_bn_buffers(), ref.flat_bn_buffers())
+        assert torch.equal(fb.adam[0].state, tr.adam.state)
+        return
+    assert_params_close({k: p.detach().cpu().numpy() for k, p in m.named_parameters()},
+                        {k: p.detach().cpu().numpy() for k, p in ref.named_parameters()}, steps=3,
+                        rtol=1e-4, atol_frac=1e-4, prefix="fold launch vs FusedTrainer ")
+    from golden_util import assert_close
+    bm, br = dict(m.named_buffers()), dict(ref.named_buffers())
+    for k in ("temporal.1.running_mean", "temporal.1.running_var", "block_2.2.running_mean",
+              "block_2.2.running_var"):
+        assert_close(bm[k].cpu().numpy(), br[k].cpu().numpy(), atol_frac=1e-4, name=k)
+    assert torch.equal(m.flat_num_batches_tracked(), ref.flat_num_batches_tracked())
 
 
 def test_graph_replay_equals_eager():
@@ -140,10 +163,11 @@ def test_step_keyed_dropout_changes_every_step():
 
 
 def test_protocol_fold_batch_matches_one_at_a_time():
-    """train.py's protocol runner: _run_folds (FoldBatch, graphs) against _run_fold (the
-    reference-shaped train() + evaluate_model() loop, model.py:101-227) on the same units.  With
-    p = 0 the dropout keying is moot, so the trained weights must agree bit for bit and the
-    reported accuracies exactly; validation losses agree to fp32 rounding (batch-mean order)."""
+    """train.py's protocol runner: _run_folds (FoldBatch, fold-indexed launches, graphs) against
+    _run_fold (the reference-shaped train() + evaluate_model() loop, model.py:101-227) on the same
+    units.  With p = 0 the dropout keying is moot; the two split each batch over different
+    workgroup counts, so weights agree to fp32 rounding and accuracies to one trial; a second
+    fold-batched run reproduces the first bit for bit."""
     import importlib
     T_ = importlib.import_module("eegnetreplication_amd.train")   # (the package exports train())
     dev = _dev()
@@ -155,14 +179,22 @@ def test_protocol_fold_batch_matches_one_at_a_time():
         ids = rng.permutation(150)
         te = (rng.standard_normal((40, C, T)), rng.integers(0, 4, 40).astype(np.int64))
         specs.append((X, y, ids[:100], ids[100:], te, 0.0, 10 + u))
+    from golden_util import assert_params_close
     batched = T_._run_units(specs, 3, dev, fold_batch=3)
     single = T_._run_units(specs, 3, dev, fold_batch=0)
     for k, (a, b) in enumerate(zip(batched, single)):
-        assert a["test_acc"] == b["test_acc"], k
-        assert a["val_acc"] == b["val_acc"], k
-        assert abs(a["val_loss"] - b["val_loss"]) <= 1e-5 * abs(b["val_loss"]), k
+        # one trial of 40 / 50 may flip on fp32 rounding of the fold launch's partial sums
+        assert abs(a["test_acc"] - b["test_acc"]) <= 100 / 40 + 1e-9, k
+        assert abs(a["val_acc"] - b["val_acc"]) <= 100 / 50 + 1e-9, k
+        assert abs(a["val_loss"] - b["val_loss"]) <= 1e-4 * abs(b["val_loss"]), k
+        assert_params_close({n: a["state"][n].numpy() for n in PARAMS},
+                            {n: b["state"][n].numpy() for n in PARAMS}, steps=6, rtol=1e-4,
+                            atol_frac=1e-4, prefix=f"unit {k} ")
+    again = T_._run_units(specs, 3, dev, fold_batch=3)    # fold batches are bit-reproducible
+    for a, b in zip(batched, again):
+        assert a["test_acc"] == b["test_acc"] and a["val_loss"] == b["val_loss"]
         for n in b["state"]:
-            assert torch.equal(a["state"][n], b["state"][n]), f"unit {k}: {n} differs"
+            assert torch.equal(a["state"][n], b["state"][n])
 
 
 @pytest.mark.parametrize("sizes", [[64, 30, 128], [1, 65]])
@@ -191,8 +223,8 @@ def test_graph_fold_edge_sizes(sizes):
 @pytest.mark.parametrize("graphs", [False, True])
 def test_fused_fold_launch_equals_per_fold_streams(graphs):
     """eegnet_train_step_folds (all folds in one launch per pass, fold = grid y) against the same
-    folds advanced on one stream each: identical parameters, BN buffers, counters, Adam state and
-    loss sums, epoch after epoch (equal-size folds, a short last batch, p = 0.5)."""
+    folds each in a one-fold fold-indexed launch: identical parameters, BN buffers, counters, Adam
+    state and loss sums, epoch after epoch (equal-size folds, a short last batch, p = 0.5)."""
     from eegnetreplication_amd import FoldBatch
     dev = _dev()
     K, n = 5, 150
@@ -201,16 +233,16 @@ def test_fused_fold_launch_equals_per_fold_streams(graphs):
     models = _models(K, 0.5, dev)
     twins = [_clone(m, 0.5, dev) for m in models]
     fused = FoldBatch(models, seeds, graphs=graphs, fused=True)
-    split = FoldBatch(twins, seeds, graphs=graphs, fused=False)
+    alone = [FoldBatch([t], [s], graphs=graphs, fused=True) for t, s in zip(twins, seeds)]
     gf = [torch.Generator().manual_seed(s) for s in seeds]
     gs = [torch.Generator().manual_seed(s) for s in seeds]
     for e in range(3):
         sf = fused.epoch(data, 64, gf)
-        ss = split.epoch(data, 64, gs)
+        ss = [fb.epoch([data[k]], 64, [gs[k]])[0] for k, fb in enumerate(alone)]
         torch.cuda.synchronize()
         for k in range(K):
             assert torch.equal(sf[k], ss[k]), f"epoch {e} fold {k}: loss sums differ"
-            for a, b in zip(_state(fused, k), _state(split, k)):
-                assert torch.equal(a, b), f"epoch {e} fold {k}: fused launch differs from per-fold streams"
+            for a, b in zip(_state(fused, k), _state(alone[k], 0)):
+                assert torch.equal(a, b), f"epoch {e} fold {k}: 5-fold launch differs from the fold alone"
     assert fused._fz is not None and (fused._fz["graph"] is not None) == graphs
     assert int(fused.adam[0].step.item()) == 3 * 3

@@ -100,6 +100,23 @@ def test_train_and_evaluate_signatures():
     assert list(inspect.signature(evaluate_model).parameters)[:2] == ["model", "test_loader"]
 
 
+def test_flat_layout_follows_replaced_parameters_and_buffers():
+    """The flat ABI buffers track the module: a newly assigned Parameter or a rebound ``.data`` is
+    re-homed into the flat parameter buffer before the next kernel reads it."""
+    m = EEGNet(22, 256)
+    flat0 = m.flat_parameters()
+    o = 8 * 32 + 8 + 8                                    # offset of spatial.weight (ABI order)
+    m.spatial.weight = nn.Parameter(torch.full_like(m.spatial.weight, 0.75))
+    flat1 = m.flat_parameters()
+    assert flat1.data_ptr() != flat0.data_ptr()
+    assert torch.all(flat1[o:o + 16 * 22] == 0.75)
+    assert m.spatial.weight.data_ptr() == flat1.data_ptr() + 4 * o
+    m.classifier.bias.data = torch.arange(4, dtype=torch.float32)
+    assert torch.equal(m.flat_parameters()[-4:], torch.arange(4, dtype=torch.float32))
+    m.aggregation[0].running_var = torch.full((16,), 2.0)
+    assert torch.all(m.flat_bn_buffers()[32:48] == 2.0)       # rm1 rv1 (8 each), rm2, rv2 (16 each)
+
+
 def test_cpu_tensors_raise_instead_of_falling_back():
     model = EEGNet(C=C, T=T)
     with pytest.raises(RuntimeError, match="HIP device"):

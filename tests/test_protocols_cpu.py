@@ -156,3 +156,54 @@ def test_fold_batches_are_balanced(monkeypatch):
     seen.clear()
     assert T_._run_units(list(range(10)), 1, "cpu", 4) == list(range(10))
     assert seen == [4, 4, 2]
+
+
+def _fake_unit(spec):
+    """A stand-in unit result that depends only on the unit's spec (as a seeded fold does)."""
+    X, y, tr_ids, va_ids, te, p, seed = spec
+    return {"test_acc": float(seed) + 0.5, "val_acc": float(len(tr_ids)), "val_loss": p,
+            "state": {"w": np.full(3, seed)}}
+
+
+def test_failed_unit_is_retried_from_a_fresh_state(monkeypatch):
+    """a fold is an idempotent unit and is re-run on a host-side failure.  One unit fails
+    once (one at a time), and one fold batch fails once (fold-batched); both runs complete with the
+    results of a run without failures.  A device fault is not retried."""
+    import pytest
+    from eegnetreplication_amd import train as T_
+    specs = [(None, None, list(range(10 + u)), [], None, 0.5, 100 + u) for u in range(5)]
+    ref = [_fake_unit(sp) for sp in specs]
+    calls = {"n": 0}
+
+    def flaky_fold(X, y, tr_ids, va_ids, te, p, epochs, seed, device):
+        calls["n"] += 1
+        if seed == 102 and calls.setdefault("failed", 0) == 0:
+            calls["failed"] = 1
+            raise RuntimeError("injected host-side failure")
+        return _fake_unit((X, y, tr_ids, va_ids, te, p, seed))
+
+    monkeypatch.setattr(T_, "_run_fold", flaky_fold)
+    got = T_._run_units(specs, 1, "cpu", fold_batch=0)
+    assert calls["failed"] == 1 and calls["n"] == 6
+    assert [r["test_acc"] for r in got] == [r["test_acc"] for r in ref]
+
+    state = {"failed": 0, "batches": []}
+
+    def flaky_folds(batch, epochs, device):
+        state["batches"].append([sp[6] for sp in batch])
+        if state["failed"] == 0 and any(sp[6] == 103 for sp in batch):
+            state["failed"] = 1
+            raise ValueError("injected failure inside a fold batch")
+        return [_fake_unit(sp) for sp in batch]
+
+    monkeypatch.setattr(T_, "_run_folds", flaky_folds)
+    got = T_._run_units(specs, 1, "cpu", fold_batch=3)
+    assert state["batches"] == [[100, 101, 102], [103, 104], [103, 104]]
+    assert [r["test_acc"] for r in got] == [r["test_acc"] for r in ref]
+
+    def gpu_fault(batch, epochs, device):
+        raise RuntimeError("HIP error: an illegal memory access was encountered")
+
+    monkeypatch.setattr(T_, "_run_folds", gpu_fault)
+    with pytest.raises(RuntimeError, match="HIP error"):
+        T_._run_units(specs, 1, "cpu", fold_batch=3)
