@@ -24,8 +24,6 @@ def _dev():
 
 # EEGNet-16,4 (F2 = 64: G5_F16D4 at 22 x 256, G5_16x4_64x512 = BASELINE cfg5) runs the o-chunked
 # wide passes (csrc/eegnet_wide.hip); every other fixture the F2 <= 16 passes.
-def _check_supported(name):
-    pass
 
 
 def _model_from(g: Golden, dev):
@@ -39,7 +37,6 @@ def _model_from(g: Golden, dev):
 @pytest.mark.parametrize("name", TRAIN_FIXTURES)
 def test_train_step_matches_reference(name):
     dev = _dev()
-    _check_supported(name)
     g = Golden(name)
     m = g.meta
     model = _model_from(g, dev).train()
