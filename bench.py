@@ -385,42 +385,59 @@ def bench_infer_bf16(dev, B, C, T, F1, D, steps, warmup):
     }
 
 
-def bench_folds(dev, n_folds, n_train, epochs):
-    """SURVEY 8(f) row 1 leg: the real training protocol (batch 64, 22 x 257 trials, EEGNet-8,2,
-    p=0.5; train.py:87,229) with n_folds independent cross-subject-sized folds (1,440 training
-    trials each, train.py:182-231) resident at once and advanced in lock-step by FoldBatch, against
-    the same folds trained one after another (the reference's order).  Synthetic data in HBM."""
+def bench_folds(dev, n_folds, n_train, epochs, rank=0, world=1, barrier=lambda: None):
+    """SURVEY 8(f) row 1 / BASELINE configs[2] leg: the real training protocol (batch 64, 22 x 257
+    trials, EEGNet-8,2, p=0.5; train.py:87,229) with n_folds independent cross-subject-sized folds
+    (1,440 training trials each, train.py:182-231), dealt to the ranks by lpt_assign (cfg3: fold
+    sharding, no communication) and trained on each rank as ONE fold batch (FoldBatch: fold-indexed
+    launches, the epoch captured as one hipGraph).  `value` = all folds' trials / the slowest rank's
+    time.  At world 1 the same folds per-fold-streamed and one after another (the reference's order)
+    are timed beside it.  Synthetic data in HBM.  Runs on every rank; returns rank 0's record."""
     from eegnetreplication_amd import EEGNet, FoldBatch
+    from eegnetreplication_amd.distributed import lpt_assign
     C, T = 22, 257
     rng = np.random.default_rng(77)
     X = torch.from_numpy(rng.standard_normal((n_train, C, T), dtype=np.float32)).to(dev)
     y = torch.from_numpy(rng.integers(0, 4, n_train)).to(dev)
+    mine = lpt_assign([1.0] * n_folds, world)[rank] if world > 1 else list(range(n_folds))
     torch.manual_seed(3)
-    models = [EEGNet(C, T, p=0.5).to(dev).train() for _ in range(n_folds)]
+    models = {k: EEGNet(C, T, p=0.5).to(dev).train() for k in mine}
 
-    def run(batches, ep):
-        gens = [[torch.Generator().manual_seed(100 + k)] for k in range(n_folds)]
-        for fb, ks in batches:                                  # warm-up epoch (workspaces)
-            fb.epoch([(X, y)] * len(ks), 64, [gens[k][0] for k in ks])
+    def run(batches, ep, sync=False):
+        gens = {k: torch.Generator().manual_seed(100 + k) for k in mine}
+        for fb, ks in batches:                                  # warm-up epoch (workspaces, graphs)
+            fb.epoch([(X, y)] * len(ks), 64, [gens[k] for k in ks])
         torch.cuda.synchronize()
+        if sync:
+            barrier()
         t0 = time.perf_counter()
         for _ in range(ep):
             for fb, ks in batches:
-                fb.epoch([(X, y)] * len(ks), 64, [gens[k][0] for k in ks])
+                fb.epoch([(X, y)] * len(ks), 64, [gens[k] for k in ks])
         torch.cuda.synchronize()
-        return n_folds * n_train * ep / (time.perf_counter() - t0)
+        if sync:
+            barrier()
+        return time.perf_counter() - t0
 
-    ks = list(range(n_folds))
-    fused = run([(FoldBatch(models, ks, graphs=True, fused=True), ks)], epochs)
-    streams = run([(FoldBatch(models, ks, graphs=True, fused=False), ks)], epochs)
-    alone = run([(FoldBatch([m], [k], fused=False), [k]) for k, m in enumerate(models)], epochs)
-    return {"metric": "real-protocol train trials/sec, batch 64, EEGNet-8,2 22ch x 257",
-            "value": round(fused, 1), "unit": "trials/s", "folds": n_folds,
-            "train_trials_per_fold": n_train, "epochs": epochs,
-            "mode": "fold-indexed launches (eegnet_train_step_folds: fold = grid y), epoch captured "
-                    "as one hipGraph",
-            "per_fold_streams_graphed_value": round(streams, 1),
-            "sequential_folds_value": round(alone, 1), "speedup": round(fused / alone, 2)}
+    dt = run([(FoldBatch([models[k] for k in mine], mine, graphs=True, fused=True), mine)], epochs, sync=True)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    fused = n_folds * n_train * epochs / float(t.item())
+    out = {"metric": "real-protocol train trials/sec, batch 64, EEGNet-8,2 22ch x 257",
+           "value": round(fused, 1), "unit": "trials/s", "folds": n_folds, "n_gpus": world,
+           "folds_per_gpu": len(mine), "train_trials_per_fold": n_train, "epochs": epochs,
+           "scaling": "strong (the folds are dealt to the ranks, no communication)",
+           "mode": "fold-indexed launches (eegnet_train_step_folds: fold = grid y), epoch captured "
+                   "as one hipGraph"}
+    if world == 1:
+        streams = n_folds * n_train * epochs / run(
+            [(FoldBatch([models[k] for k in mine], mine, graphs=True, fused=False), mine)], epochs)
+        alone = n_folds * n_train * epochs / run(
+            [(FoldBatch([models[k]], [k], fused=False), [k]) for k in mine], epochs)
+        out.update({"per_fold_streams_graphed_value": round(streams, 1),
+                    "sequential_folds_value": round(alone, 1), "speedup": round(fused / alone, 2)})
+    return out if rank == 0 else None
 
 
 def bench_cfg4(dev, rank, world, G, steps, warmup, barrier, nx=2):
@@ -536,6 +553,9 @@ def main():
     cfg4 = None
     if not args.no_cfg4:
         cfg4 = bench_cfg4(dev, rank, world, args.global_batch, steps=10, warmup=3, barrier=barrier)
+    folds = None
+    if not args.no_folds:
+        folds = bench_folds(dev, args.folds, 1440, 2, rank, world, barrier)
     if rank == 0:
         ab = kernel_alg_bytes(C, T)
         per_kernel = kernel_table(table, alg, B, ab)
@@ -550,9 +570,6 @@ def main():
         infer = None
         if not args.no_infer:
             infer = bench_infer_bf16(dev, args.infer_batch, 64, 512, 16, 4, steps=20, warmup=3)
-        folds = None
-        if not args.no_folds:
-            folds = bench_folds(dev, args.folds, 1440, epochs=2)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu, real_cpu = cpu_baselines(C, T, B, args.cpu_steps)

@@ -771,12 +771,14 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
 }  // extern "C"
 
 // trials per workgroup of the fold-indexed launches: streaming passes A / B / E, passes C / D, the
-// whole-trial block-2 passes (EEGNET_B2=1).  The defaults reproduce the 90-fold real-protocol grids
-// of a batch of 64 (5 / 2 / 11 workgroups per fold); EEGNET_FOLD_TPW="s,c,b2" overrides them (sweeps).
+// whole-trial block-2 passes (EEGNET_B2=1); EEGNET_FOLD_TPW="s,c,b2" overrides them (sweeps).  Chosen
+// by tools/fold_tpw_sweep.py over 90, 36 and 12 resident folds of batch 64 (22 x 257):
+// 4,8,2 trains 12 folds per GPU (cfg3: 90 folds over 8 GPUs) 1.9x faster than the grid 90 folds on
+// one GPU prefer (13,32,6), at 7 % less on those 90.
 static void fold_tpw(int* s, int* c, int* b2) {
     static int v[3] = {0, 0, 0};
     if (v[0] == 0) {
-        int a = 13, b = 32, d = 6;
+        int a = 4, b = 8, d = 2;
         if (const char* e = getenv("EEGNET_FOLD_TPW")) {
             int x = 0, y = 0, z = 0;
             if (sscanf(e, "%d,%d,%d", &x, &y, &z) == 3 && x > 0 && y > 0 && z > 0) { a = x; b = y; d = z; }

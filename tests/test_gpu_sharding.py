@@ -46,7 +46,8 @@ def _np_state(sd):
 
 
 def _run(protocol, max_units):
-    from eegnetreplication_amd import train as T_
+    import importlib
+    T_ = importlib.import_module("eegnetreplication_amd.train")    # (the package exports train())
     if protocol == "ws":
         per_subject, avg, states = T_.within_subject_training(EPOCHS, 0, "cuda:0", 90, max_units)
         return per_subject, avg, [_np_state(s) for s in states]
