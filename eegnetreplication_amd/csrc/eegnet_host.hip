@@ -67,6 +67,26 @@ static bool use_b2_narrow(const Geo&) {
     return v == 1;
 }
 
+// workgroups per CU slot of the streaming passes A / B / E (EEGNET_GRIDS_MULT, experiments): with more
+// workgroups than resident slots the dispatcher refills a CU's early-finishing slot, so the two
+// resident workgroups' skew turns into load balance
+static int env_mult(const char* name) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : 1;
+    return (v >= 1 && v <= 8) ? v : 1;
+}
+static int grid_mult() {
+    static int m = 0;
+    if (m == 0) m = env_mult("EEGNET_GRIDS_MULT");
+    return m;
+}
+// the same for passes C / D (EEGNET_GRIDC_MULT)
+static int grid_mult_cd() {
+    static int m = 0;
+    if (m == 0) m = env_mult("EEGNET_GRIDC_MULT");
+    return m;
+}
+
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     if (!d) return fail(EEGNET_EINVAL, "dims is NULL");
     memset(g, 0, sizeof(*g));
@@ -113,8 +133,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nC = NCLS * g->NF + NCLS + 2 * g->F2 + 1;
     g->nD = g->F2 * g->F2 + 18 * g->F2;
     g->nE = g->F2 * g->K1 + g->F2 * g->C + 2 * g->F2;
-    g->grid = std::min(g->B, device_cus());             // passes C, D, infer
-    g->gridS = std::min(g->B, device_cus() * WGPC);     // streaming passes A, B, E
+    g->grid = std::min(g->B, device_cus() * grid_mult_cd());     // passes C, D, infer
+    g->gridS = std::min(g->B, device_cus() * WGPC * grid_mult());     // streaming passes A, B, E
     const int rows1 = g->C * g->RS;                   // x rows (one buffer)
     const int nf4 = rup(g->NF, 4);
     g->ldsA = rows1 + g->F2 * g->RS + NWB * (g->K1 + 1);
@@ -315,7 +335,7 @@ static void ensure_attrs() {
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
                           (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>,
-                          (const void*)k_infer_bf16<8, true>})
+                          (const void*)k_infer_bf16<8, true>, (const void*)k_infer_bf16_cfg5})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 0, 0, 0>();
     set_attrs_shape<64, 0, 0, 0>();
@@ -700,7 +720,12 @@ int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const
     const dim3 grid(std::min(g.B, device_cus())), blk(NTI);
     PROF(KID_INFER_BF16);
     if (same_geo_bf16(g, kGeoCfg5)) {
-        hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
+        // time-chunked cfg5 kernel, two workgroups per CU (eegnet_infer_bf16c.hip); EEGNET_BF16_V1=1
+        // keeps the whole-trial kernel (A/B measurements)
+        static const bool v1 = getenv("EEGNET_BF16_V1") && getenv("EEGNET_BF16_V1")[0] == '1';
+        if (v1) hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
+        else hipLaunchKernelGGL(k_infer_bf16_cfg5, dim3(std::min(g.B, 2 * device_cus())), dim3(c5::NT), c5::LDS, s,
+                                g, params, bn_buffers, x, logits);
         LAUNCH_CHECK("k_infer_bf16(cfg5)");
         return 0;
     }

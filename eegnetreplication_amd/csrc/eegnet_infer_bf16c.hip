@@ -1,0 +1,319 @@
+// eegnet_infer_bf16c.hip -- bf16 batched eval forward of BASELINE cfg5 (EEGNet-16,4 on 64ch x 512),
+// time-chunked so that two trials are resident per CU.  Included by eegnet_kernels.hip.
+//
+// Same arithmetic as k_infer_bf16 (eegnet_infer_bf16.hip: BN-folded spatial GEMM, 32-tap FIR, folded
+// BN1/BN2 + ELU + pool4, depthwise 1x16, pointwise, BN3 + ELU + pool8, classifier; bf16 operands, fp32
+// accumulation; reference: EEGNet.forward in eval mode, src/eegnet_repl/model.py:91-99).  What changes
+// is the data flow, for occupancy:
+//
+// * k_infer_bf16 keeps a whole trial's x image (64 KB) and s rows (72 KB) in LDS, so one 8-wave
+//   workgroup fits a CU and every SIMD runs the same phase at the same time.  Here a trial is cut into
+//   NCH = 8 time chunks of TC = 64 output samples: a chunk's x image (96 samples incl. the 'same'
+//   halo, 16 KB, two buffers) and s rows (12 KB) are all the full-rate data in LDS, and the pooled
+//   rows a (bf16, 18 KB) accumulate over the chunks.  74 KB per workgroup: two workgroups (16 waves)
+//   per CU, on different trials and out of phase.
+// * x arrives by LDS-DMA (global_load_lds_dwordx4) straight into the XOR-swizzled transposed-read
+//   image -- the swizzle is applied to the per-lane SOURCE address, the 16-byte units of a wave land
+//   contiguously -- two chunks ahead, with no prefetch registers (<= 128 VGPRs for 4 waves / SIMD).
+// * FIR on the matrix cores with a full MFMA per chunk: the 16 columns are (row r of a temporal
+//   group, 16-sample tile) -- the D = 4 rows of a group share the banded Toeplitz A operand of the
+//   group's taps -- so a 64-sample chunk still fills all 16 columns.
+// * depthwise 1x16 on the matrix cores too (banded Toeplitz of the row's 16 taps, K = 32 window;
+//   8 of 16 columns used), instead of 131 K VALU FMAs per trial.
+namespace eeg {
+namespace c5 {
+
+constexpr int C = 64, T = 512, F1 = 16, D = 4, F2 = 64, K1 = 32, T1 = 128, T2 = 16, NF = F2 * T2;
+constexpr int TC = 64;                       // output samples per chunk: D rows x TC/16 tiles = 16 columns
+constexpr int NCH = T / TC;                  // chunks per trial
+constexpr int NTS = 6;                       // spatial 16-sample tiles per chunk (64j - 16 .. 64j + 80)
+constexpr int XROWB = 256;                   // x image row (bytes): 128 bf16, 96 used; swizzle needs 128
+constexpr int XIMG = C * XROWB;              // 16 KB per chunk buffer
+constexpr int SROW = 120;                    // s row stride (bf16): 112 read, 60 dwords = 4 mod 8
+constexpr int AROW = 144;                    // a row (bf16): [8 zeros | 128 pooled | 8 zeros]
+constexpr int W2R = 48;                      // depthwise taps, bf16, [16 zeros | 16 taps | 16 zeros]
+constexpr int NT = 512;                      // threads: 8 waves
+constexpr int NW = NT / 64;
+// LDS carve (bytes)
+constexpr int OFF_X0 = 0, OFF_X1 = XIMG, OFF_S = 2 * XIMG;
+constexpr int OFF_A = OFF_S + F2 * SROW * 2;
+constexpr int OFF_W1 = OFF_A + F2 * AROW * 2;
+constexpr int OFF_W2 = OFF_W1 + F1 * K1 * 4;
+constexpr int OFF_CO = OFF_W2 + F2 * W2R * 2;
+constexpr int OFF_LG = OFF_CO + 4 * F2 * 4;
+constexpr int LDS = OFF_LG + NW * NCLS * 4;
+static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+static_assert(F2 % 16 == 0 && 16 % D == 0 && TC == 16 * (16 / D), "FIR columns = rows of a group x tiles");
+
+}  // namespace c5
+
+__device__ __attribute__((aligned(16))) uint32_t g_zero16[4] = {0u, 0u, 0u, 0u};   // DMA source of the pads
+
+// LDS-DMA of one 16-byte unit per lane (wave-instruction: 64 units, 1 KiB contiguous at ldst), from
+// inline asm so the compiler's waitcnt pass does not treat it as an LDS write (eegnet_stream.hip dma16)
+__device__ __forceinline__ void dma16c(const void* gsrc, const void* ldst) {
+    const unsigned la = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)ldst;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(gsrc), "s"(la) : "memory", "m0");
+}
+
+// chunk j of trial xb (bf16 [C][T]) into an x image: samples 64j - 16 .. 64j + 79 of every channel row,
+// 16-byte units u = 0..11 of the row; physical unit u' of row r holds unit u' ^ 2h(r) (trimg_off's 8-byte
+// chunk swizzle ch ^ 4h, on unit pairs).  Units outside the trial read zeros ('same' padding).  Each
+// wave issues 2 wave-instructions (4 rows each).
+__device__ __forceinline__ void x_chunk_dma(const uint16_t* __restrict__ xb, int j, char* img, int wave, int lane) {
+    using namespace c5;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r0 = 4 * (wave + NW * i);
+        const int r = r0 + (lane >> 4), up = lane & 15;
+        const int h = (r & 3) | ((r >> 1) & 4);
+        const int u = up ^ (2 * h);
+        if (u < 12) {
+            const int s0 = TC * j - 16 + 8 * u;
+            const void* src = (s0 >= 0 && s0 < T) ? (const void*)(xb + (size_t)r * T + s0) : (const void*)g_zero16;
+            dma16c(src, img + r0 * XROWB);
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void barrier_vm_c() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(N) : "memory");
+}
+__device__ __forceinline__ void barrier_lds_c() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// __launch_bounds__ second argument: minimum waves per SIMD (4: two 8-wave workgroups per CU, <= 128 VGPRs)
+__global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const float* __restrict__ prm,
+                                                               const float* __restrict__ bn,
+                                                               const uint16_t* __restrict__ x,
+                                                               float* __restrict__ logits) {
+    using namespace c5;
+    extern __shared__ __attribute__((aligned(16))) char smc[];
+    char* const Si = smc + OFF_S;                       // s rows (bf16) of the current chunk
+    char* const Ai = smc + OFF_A;                       // pooled rows a (bf16), whole trial
+    char* const Zi = smc + OFF_X1;                      // z image (bf16, swizzled): x buffer 1 after chunk 7
+    float* const W1t = reinterpret_cast<float*>(smc + OFF_W1);
+    uint16_t* const W2p = reinterpret_cast<uint16_t*>(smc + OFF_W2);
+    float* const Co = reinterpret_cast<float*>(smc + OFF_CO);   // [4][F2]: al, be, s3, b3
+    float* const Lg = reinterpret_cast<float*>(smc + OFF_LG);   // [NW][4] logit partials
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int G = lane >> 4, l15 = lane & 15;
+    const int B = g.B;
+
+    // ---- prologue: next x DMA first (the tables below overlap it), then tables and zero pads ----
+    int b = blockIdx.x;
+    if (b < B) {
+        x_chunk_dma(x + (size_t)b * C * T, 0, smc + OFF_X0, wave, lane);
+        x_chunk_dma(x + (size_t)b * C * T, 1, smc + OFF_X1, wave, lane);
+    }
+    if (tid < F2) {
+        const int o = tid, gg = o / D;
+        const float* rm1 = bn;             const float* rv1 = bn + F1;
+        const float* rm2 = bn + 2 * F1;    const float* rv2 = rm2 + F2;
+        const float* rm3 = rm2 + 2 * F2;   const float* rv3 = rm3 + F2;
+        const float a1 = prm[g.o_g1 + gg] / sqrtf(rv1[gg] + g.eps);
+        const float c1 = prm[g.o_b1 + gg] - a1 * rm1[gg];
+        float W = 0.f;
+        for (int c = 0; c < C; ++c) W += prm[g.o_ws + o * C + c];
+        const float s2 = prm[g.o_g2 + o] / sqrtf(rv2[o] + g.eps);
+        const float s3 = prm[g.o_g3 + o] / sqrtf(rv3[o] + g.eps);
+        Co[o] = a1 * s2;
+        Co[F2 + o] = (c1 * W - rm2[o]) * s2 + prm[g.o_b2 + o];
+        Co[2 * F2 + o] = s3;
+        Co[3 * F2 + o] = prm[g.o_b3 + o] - rm3[o] * s3;
+    }
+    for (int i = tid; i < F1 * K1; i += NT) W1t[i] = prm[g.o_w1 + i];
+    for (int i = tid; i < F2 * W2R; i += NT) {
+        const int o = i / W2R, k = i - o * W2R - 16;
+        W2p[i] = __builtin_bit_cast(uint16_t, (__bf16)((k >= 0 && k < K2) ? prm[g.o_w2 + o * K2 + k] : 0.f));
+    }
+    // s rows: positions 96..111 meet only zero taps but must be finite; a rows: 'same' pads of the dw16
+    for (int i = tid; i < F2 * SROW / 2; i += NT) reinterpret_cast<uint32_t*>(Si)[i] = 0u;
+    for (int i = tid; i < F2 * AROW / 2; i += NT) reinterpret_cast<uint32_t*>(Ai)[i] = 0u;
+
+    // spatial GEMM: this wave's o-tile (ws^T B operand, K = c, both K-steps in registers) and t-tiles
+    const int ot = wave & 3, tt0 = wave >> 2;
+    bf16x8 wsf[2];
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+            wsf[kc][jj] = (__bf16)prm[g.o_ws + (ot * 16 + l15) * C + kc * 32 + 8 * G + jj];
+    // pointwise A operand (W3, K = i): the same o-tile of output rows j
+    bf16x8 w3f[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+            w3f[ks][jj] = (__bf16)prm[g.o_W3 + (ot * 16 + l15) * F2 + ks * 32 + 8 * G + jj];
+    __syncthreads();                                   // tables (not the DMA: asm, waited per chunk)
+
+    // FIR: this wave's two temporal groups gi = 2 wave + {0, 1}; banded Toeplitz A operand of each
+    // group's taps, A[i][j] = w1[g][j - i - 1] over K = 64 (two K-steps), held for the whole kernel;
+    // this lane's FIR column is (row r = l15 >> 2 of the group, tile l15 & 3)
+    bf16x8 af[2][2];
+    float al2[2], be2[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int gg = 2 * wave + q;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const int k = 32 * s + 8 * G + jj - l15 - 1;
+                af[q][s][jj] = (__bf16)((k >= 0 && k < K1) ? W1t[gg * K1 + k] : 0.f);
+            }
+        const int o = D * gg + (l15 >> 2);
+        al2[q] = Co[o] * 1.4426950408889634f;              // ELU in log2 units (k_infer_bf16)
+        be2[q] = Co[F2 + o] * 1.4426950408889634f;
+    }
+    // pointwise epilogue constants of this lane's 4 output rows j = ot*16 + 4G + rr
+    float s3r[4], b3r[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+        s3r[rr] = Co[2 * F2 + ot * 16 + 4 * G + rr];
+        b3r[rr] = Co[3 * F2 + ot * 16 + 4 * G + rr];
+    }
+    const float* Wf = prm + g.o_Wfc;
+#ifdef EEGNET_TRACE
+    // traced build (tools/trace_bf16.py): thread 0's shader cycles per phase, summed over the trials
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_ = clock64();
+#define PH_(k) do { if (g.dbg && tid == 0) { const unsigned long long t1_ = clock64(); ph[k] += t1_ - t_; t_ = t1_; } } while (0)
+#else
+#define PH_(k) do {} while (0)
+#endif
+
+    for (; b < B; b += gridDim.x) {
+        const bool more = b + (int)gridDim.x < B;
+        const uint16_t* xn = x + (size_t)(b + gridDim.x) * C * T;
+#pragma unroll 1
+        for (int j = 0; j < NCH; ++j) {
+            char* const Xi = smc + ((j & 1) ? OFF_X1 : OFF_X0);
+            // x chunk j landed (every wave's DMAs; each wave has 2 newer ones in flight unless none was
+            // issued after: chunk 7 of the last trial); the previous chunk's FIR is done with Si
+            if (j < NCH - 1 || more) barrier_vm_c<2>();
+            else barrier_vm_c<0>();
+            PH_(0);
+            // ---- 1. spatial GEMM s^T[t][o] (16 t x 16 o tiles, A = x^T by transposed reads) ----
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const int n = tt0 + 2 * m;
+                const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
+                const bf16x8 a0 = tr_frag(Xi, XROWB, 0, 16 * n, lane), a1 = tr_frag(Xi, XROWB, 32, 16 * n, lane);
+                floatx4 acc = mfma_bf16(a0, wsf[0], z4);
+                acc = mfma_bf16(a1, wsf[1], acc);
+                uintx2 pk;
+                pk[0] = pack_bf16x2(acc[0], acc[1]);
+                pk[1] = pack_bf16x2(acc[2], acc[3]);
+                *reinterpret_cast<uintx2*>(Si + (ot * 16 + l15) * (2 * SROW) + 2 * (16 * n + 4 * G)) = pk;
+            }
+            PH_(1);
+            barrier_lds_c();                               // s rows complete; x buffer consumed
+            PH_(2);
+            if (j + 2 < NCH) x_chunk_dma(x + (size_t)b * C * T, j + 2, Xi, wave, lane);
+            else if (j == NCH - 2 && more) x_chunk_dma(xn, 0, Xi, wave, lane);   // next trial's chunk 0
+            // ---- 2. FIR (banded Toeplitz MFMA), folded BN, ELU, pool4 -> a rows ----
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int gg = 2 * wave + q;
+                const int o = D * gg + (l15 >> 2), tile = l15 & 3;
+                const char* srw = Si + o * (2 * SROW) + 2 * (16 * tile + 8 * G);
+                floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+                acc = mfma_bf16(af[q][0], *reinterpret_cast<const bf16x8*>(srw), acc);
+                acc = mfma_bf16(af[q][1], *reinterpret_cast<const bf16x8*>(srw + 64), acc);
+                // lane: v[o][t = 64j + 16 tile + 4G + r]; pooled sample 16j + 4 tile + G
+                float pp = 0.f, pn = 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float y = fmaf(al2[q], acc[r], be2[q]);
+                    pp += fmaxf(y, 0.f);
+                    pn += __builtin_amdgcn_exp2f(fminf(y, 0.f));
+                }
+                const float a = fmaf(0.25f * 0.6931471805599453f, pp, 0.25f * pn - 1.f);
+                reinterpret_cast<__bf16*>(Ai)[o * AROW + 8 + 16 * j + 4 * tile + G] = (__bf16)a;
+            }
+            PH_(3);
+        }
+        barrier_lds_c();                                   // a rows complete (the 8 chunks); x buffer 1 free
+        PH_(4);
+
+        // ---- 3. depthwise 1x16 (pad 7 | 8) on the matrix cores -> z image (x buffer 1) ----
+        // z[o][16n + i] = sum_j A[i][j] W_n[j], A[i][j] = w2[o][j - i - 1], W_n[j] = a[o][16n + j - 8]
+#pragma unroll 2
+        for (int rr = 0; rr < F2 / NW; ++rr) {
+            const int o = wave * (F2 / NW) + rr;
+            const uint16_t* wp = W2p + o * W2R + 15 + 8 * G - l15;
+            bf16x8 aw;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) aw[jj] = __builtin_bit_cast(__bf16, wp[jj]);
+            const int tile = l15 & 7;
+            const bf16x8 win = *reinterpret_cast<const bf16x8*>(Ai + o * (2 * AROW) + 2 * (16 * tile + 8 * G));
+            const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
+            const floatx4 acc = mfma_bf16(aw, win, z4);
+            if (l15 < 8) {                                 // lane: z[o][16 l15 + 4G + r]
+                uintx2 pk;
+                pk[0] = pack_bf16x2(acc[0], acc[1]);
+                pk[1] = pack_bf16x2(acc[2], acc[3]);
+                *reinterpret_cast<uintx2*>(Zi + trimg_off(o, 4 * l15 + G, XROWB)) = pk;
+            }
+        }
+        PH_(5);
+        barrier_lds_c();
+        PH_(4);
+
+        // ---- 4. pointwise MFMA (A = W3, B = z by transposed reads), BN3, ELU, pool8, classifier ----
+        // (the classifier addresses hang off an opaque per-trial base: hoisted out of the trial loop
+        // they were 64 loop-invariant pointers, spilled)
+        const float* const Wfb = Wf + opaque0();
+        float lp[NCLS] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int n = tt0 + 2 * m;
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            acc = mfma_bf16(w3f[0], tr_frag(Zi, XROWB, 0, 16 * n, lane), acc);
+            acc = mfma_bf16(w3f[1], tr_frag(Zi, XROWB, 32, 16 * n, lane), acc);
+            // lane: r[j = ot*16 + 4G + rr][q = 16n + l15]; pool8 over 8 lanes of q
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                float e = elu_f(fmaf(s3r[rr], acc[rr], b3r[rr]));
+                e += __shfl_xor(e, 1, 64);
+                e += __shfl_xor(e, 2, 64);
+                e += __shfl_xor(e, 4, 64);
+                if ((lane & 7) == 0) {
+                    const float hv = 0.125f * e;
+                    const int f = (ot * 16 + 4 * G + rr) * T2 + 2 * n + (l15 >> 3);
+#pragma unroll
+                    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(Wfb[c * NF + f], hv, lp[c]);
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c) lp[c] = wave_sum(lp[c]);
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NCLS; ++c) Lg[wave * NCLS + c] = lp[c];
+        }
+        PH_(6);
+        barrier_lds_c();                                   // logit partials complete; z image consumed
+        PH_(4);
+        if (tid < NCLS) {
+            float a = prm[g.o_bfc + tid];
+            for (int w = 0; w < NW; ++w) a += Lg[w * NCLS + tid];
+            logits[(size_t)b * NCLS + tid] = a;
+        }
+        if (more) x_chunk_dma(xn, 1, smc + OFF_X1, wave, lane);  // next trial's chunk 1 (x buffer 1 is free)
+        PH_(7);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef EEGNET_TRACE
+    if (g.dbg && tid == 0)
+        for (int k = 0; k < 8; ++k) reinterpret_cast<unsigned long long*>(g.dbg)[blockIdx.x * 8 + k] = ph[k];
+#endif
+#undef PH_
+}
+
+}  // namespace eeg

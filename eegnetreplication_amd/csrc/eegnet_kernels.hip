@@ -40,4 +40,5 @@
 #include "eegnet_passes.hip"
 #include "eegnet_wide.hip"
 #include "eegnet_infer_bf16.hip"
+#include "eegnet_infer_bf16c.hip"
 #include "eegnet_host.hip"
