@@ -178,7 +178,17 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
         s3r[rr] = Co[2 * F2 + ot * 16 + 4 * G + rr];
         b3r[rr] = Co[3 * F2 + ot * 16 + 4 * G + rr];
     }
-    const float* Wf = prm + g.o_Wfc;
+    // classifier weights this lane multiplies, held for the whole kernel: after pool8 every lane of an
+    // 8-lane group holds the group's 4 pooled values (rows rr); lane p = l15 & 7 takes row rr = p >> 1
+    // and classes 2 (p & 1), 2 (p & 1) + 1, for each of its wave's 4 pointwise tiles (8 weights)
+    const int prr = (l15 & 7) >> 1, pc0 = 2 * (l15 & 1);
+    float wfl[4][2];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int f = (ot * 16 + 4 * G + prr) * T2 + 2 * (tt0 + 2 * m) + (l15 >> 3);
+        wfl[m][0] = prm[g.o_Wfc + pc0 * NF + f];
+        wfl[m][1] = prm[g.o_Wfc + (pc0 + 1) * NF + f];
+    }
 #ifdef EEGNET_TRACE
     // traced build (tools/trace_bf16.py): thread 0's shader cycles per phase, summed over the trials
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_ = clock64();
@@ -243,7 +253,7 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
 
         // ---- 3. depthwise 1x16 (pad 7 | 8) on the matrix cores -> z image (x buffer 1) ----
         // z[o][16n + i] = sum_j A[i][j] W_n[j], A[i][j] = w2[o][j - i - 1], W_n[j] = a[o][16n + j - 8]
-#pragma unroll 2
+#pragma unroll 4
         for (int rr = 0; rr < F2 / NW; ++rr) {
             const int o = wave * (F2 / NW) + rr;
             const uint16_t* wp = W2p + o * W2R + 15 + 8 * G - l15;
@@ -266,36 +276,36 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
         PH_(4);
 
         // ---- 4. pointwise MFMA (A = W3, B = z by transposed reads), BN3, ELU, pool8, classifier ----
-        // (the classifier addresses hang off an opaque per-trial base: hoisted out of the trial loop
-        // they were 64 loop-invariant pointers, spilled)
-        const float* const Wfb = Wf + opaque0();
-        float lp[NCLS] = {0.f, 0.f, 0.f, 0.f};
+        float lp0 = 0.f, lp1 = 0.f;                       // classes pc0, pc0 + 1 of this lane's row prr
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const int n = tt0 + 2 * m;
             floatx4 acc = {0.f, 0.f, 0.f, 0.f};
             acc = mfma_bf16(w3f[0], tr_frag(Zi, XROWB, 0, 16 * n, lane), acc);
             acc = mfma_bf16(w3f[1], tr_frag(Zi, XROWB, 32, 16 * n, lane), acc);
-            // lane: r[j = ot*16 + 4G + rr][q = 16n + l15]; pool8 over 8 lanes of q
+            // lane: r[j = ot*16 + 4G + rr][q = 16n + l15]; pool8 over the 8 lanes of q (every lane of
+            // the group ends with the sums)
+            float e[4];
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                float e = elu_f(fmaf(s3r[rr], acc[rr], b3r[rr]));
-                e += __shfl_xor(e, 1, 64);
-                e += __shfl_xor(e, 2, 64);
-                e += __shfl_xor(e, 4, 64);
-                if ((lane & 7) == 0) {
-                    const float hv = 0.125f * e;
-                    const int f = (ot * 16 + 4 * G + rr) * T2 + 2 * n + (l15 >> 3);
+            for (int rr = 0; rr < 4; ++rr) e[rr] = elu_f(fmaf(s3r[rr], acc[rr], b3r[rr]));
 #pragma unroll
-                    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(Wfb[c * NF + f], hv, lp[c]);
-                }
-            }
+            for (int rr = 0; rr < 4; ++rr) e[rr] += __shfl_xor(e[rr], 1, 64);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) e[rr] += __shfl_xor(e[rr], 2, 64);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) e[rr] += __shfl_xor(e[rr], 4, 64);
+            const float hv = 0.125f * (prr == 0 ? e[0] : prr == 1 ? e[1] : prr == 2 ? e[2] : e[3]);
+            lp0 = fmaf(wfl[m][0], hv, lp0);
+            lp1 = fmaf(wfl[m][1], hv, lp1);
         }
-#pragma unroll
-        for (int c = 0; c < NCLS; ++c) lp[c] = wave_sum(lp[c]);
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < NCLS; ++c) Lg[wave * NCLS + c] = lp[c];
+        {   // per class: the lanes holding it (p & 1 selects the class pair) summed over the wave
+            float lp[NCLS];
+            lp[0] = pc0 == 0 ? lp0 : 0.f;
+            lp[1] = pc0 == 0 ? lp1 : 0.f;
+            lp[2] = pc0 == 2 ? lp0 : 0.f;
+            lp[3] = pc0 == 2 ? lp1 : 0.f;
+            wave_reduce<NCLS>(lp);                        // lane 16 r holds class r in lp[0]
+            if ((lane & 15) == 0) Lg[wave * NCLS + (lane >> 4)] = lp[0];
         }
         PH_(6);
         barrier_lds_c();                                   // logit partials complete; z image consumed
