@@ -366,11 +366,11 @@ def bench_infer_bf16(dev, B, C, T, F1, D, steps, warmup):
         kern = _lib.profile_collect()
         _lib.profile_enable(False)
     cnt, tot = kern.get("k_infer_bf16", (0, 0.0))
+    # the cfg5 shape runs the time-chunked kernel (csrc/eegnet_infer_bf16c.hip), any other the generic one
+    kname = "k_infer_bf16_cfg5" if (C, T, F1, D) == (64, 512, 16, 4) else "k_infer_bf16"
     traffic = None                    # HBM bytes per launch from the committed rocprofv3 PMC passes
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path) and B == 16384:
-        with open(pmc_path) as f:
-            traffic = json.load(f).get("k_infer_bf16", {}).get("hbm_bytes_per_launch")
+    if B == 16384:
+        traffic = load_pmc().get(kname, {}).get("hbm_bytes_per_launch")
     avg_s = tot / max(cnt, 1) * 1e-3
     by, fl = INFER_BF16_BYTES(C, T), INFER_FLOP(C, T, F1 * D)
     ach = by * B / avg_s / 1e9
@@ -379,7 +379,7 @@ def bench_infer_bf16(dev, B, C, T, F1, D, steps, warmup):
         "value": round(B * steps / dt, 1), "unit": "trials/s", "batch": B, "steps": steps,
         "dtype": "bf16 operands, fp32 accumulation", "finite": bool(torch.isfinite(out).all()),
         "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": "k_infer_bf16",
+                     "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "kernel": kname,
                      "avg_us": round(avg_s * 1e6, 2), "alg_bytes_per_launch": by * B,
                      "alg_tflops": round(fl * B / avg_s / 1e12, 2)},
     }
