@@ -52,6 +52,12 @@ _SIGS = {
                                          ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp,
                                          _vp, _vp, ctypes.c_int, _vp]),
+    "eegnet_train_stage": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp,
+                                          _vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp,
+                                          ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                          _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "eegnet_stage_sums": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.c_int, ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_int)]),
     "eegnet_train_step_folds": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.c_int, _vp, ctypes.c_int64,
                                                ctypes.c_int64, ctypes.c_uint64, ctypes.c_float,
                                                ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp]),

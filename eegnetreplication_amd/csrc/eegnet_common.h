@@ -68,6 +68,10 @@ struct Geo {
     int wide, NOC, CPC, F2P, RB, gridB2;
     int splitC, splitD, splitE;   // wide passes whose reduction + finalize run in k_coltail (wide rows)
     int ldsWA, ldsWB, ldsWB2, ldsWC, ldsWD, ldsWE, ldsWI;
+    // batch the statistics and the CE mean are normalised by: B, or the global batch of a data-parallel
+    // step with synchronised BatchNorm (eegnet_train_stage), whose per-pass sums are all-reduced
+    int Bn;
+    int defer;           // the reduction's winner leaves the pass's sums in part2 row 0; no finalize
 };
 
 // timeline stamps: wall clock (100 MHz) at kernel phase boundaries, shader-clock phase sums (loop)

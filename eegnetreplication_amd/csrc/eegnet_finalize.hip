@@ -104,6 +104,10 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     __syncthreads();
     TRACE(g, tp, TR_TOP);
     TRACE_FS(g, tp, 3);
+    if (g.defer) {                 // synchronised BatchNorm: the host all-reduces the sums, then k_fin
+        for (int c = tid; c < ncols; c += nth) fa.part2[c] = S[c];
+        return false;
+    }
     return true;
 }
 
@@ -203,7 +207,7 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     for (int i = tid; i < K1 * K1 + K1; i += nth) fa.stats[i] = Gm[i];
     // BN1 moments from the quadratic forms w^T G w and w^T S1: one (filter, tap) per lane, the
     // filter's K1 lanes reduced by shuffles (G symmetric: column reads)
-    const double n1 = (double)g.B * C * g.T;
+    const double n1 = (double)g.Bn * C * g.T;
     for (int p = tid; p < F1 * K1; p += nth) {
         const int gg = p / K1, k = p - gg * K1;
         const float* w = pw1 + gg * K1;
@@ -235,7 +239,7 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     }
     __syncthreads();
     TRACE_FS(g, fa.tpass, 5);
-    const double n2 = (double)g.B * g.T;
+    const double n2 = (double)g.Bn * g.T;
     if (tid < F2) {
         const int o = tid, gg = o / g.D;
         double W = 0.0;
@@ -263,7 +267,7 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
 __device__ void fin2(const Geo& g, const double* sums, const FinArgs& fa) {
     const int j = threadIdx.x;
     if (j >= g.F2) return;
-    const double n3 = (double)g.B * g.T1;
+    const double n3 = (double)g.Bn * g.T1;
     const double mu = sums[j] / n3;
     const double var = fmax(sums[g.F2 + j] / n3 - mu * mu, 0.0);
     fa.coef[CF_MU3 * CSTR + j] = (float)mu;
@@ -288,14 +292,14 @@ __device__ void fin3(const Geo& g, const float* prm, const double* sums, const F
         const double sdz = sums[n4 + NCLS + j], sdzx = sums[n4 + NCLS + g.F2 + j];
         fa.grads[g.o_b3 + j] = (float)sdz;
         fa.grads[g.o_g3 + j] = (float)sdzx;
-        const double n3 = (double)g.B * g.T1;
+        const double n3 = (double)g.Bn * g.T1;
         const double A = (double)prm[g.o_g3 + j] * (double)fa.coef[CF_INV3 * CSTR + j];
         fa.coef[CF_A3 * CSTR + j] = (float)A;
         fa.coef[CF_B3 * CSTR + j] = (float)(-A * sdz / n3);
         fa.coef[CF_C3 * CSTR + j] = (float)(-A * sdzx / n3);
     }
     if (tid == 0 && fa.ce) {
-        const float l = (float)(sums[n4 + NCLS + 2 * g.F2] / (double)g.B);
+        const float l = (float)(sums[n4 + NCLS + 2 * g.F2] / (double)g.Bn);
         fa.coef[CF_LOSS * CSTR] = l;
         if (fa.loss) *fa.loss = l;
     }
@@ -312,7 +316,7 @@ __device__ void fin4(const Geo& g, const float* prm, const double* sums, const F
         const double sdzx = sums[g.F2 * g.F2 + 17 * g.F2 + o];
         fa.grads[g.o_b2 + o] = (float)sdz;
         fa.grads[g.o_g2 + o] = (float)sdzx;
-        const double n2 = (double)g.B * g.T;
+        const double n2 = (double)g.Bn * g.T;
         const double A = (double)prm[g.o_g2 + o] * (double)fa.coef[CF_INV2 * CSTR + o];
         fa.coef[CF_AO * CSTR + o] = (float)A;
         fa.coef[CF_BO * CSTR + o] = (float)(-A * sdz / n2);
@@ -399,7 +403,7 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     }
     __syncthreads();
     TRACE_FS(g, fa.tpass, 5);
-    const double n1 = (double)g.B * g.C * g.T;
+    const double n1 = (double)g.Bn * g.C * g.T;
     for (int p = tid; p < F1 * K1; p += nth) {
         const int gg = p / K1, k = p - gg * K1;
         const double* w = wd + gg * K1;
@@ -437,6 +441,23 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
         fa.params[i] = pp; fa.adam_m[i] = mm; fa.adam_v[i] = vv;
     }
     if (tid == 0) *fa.step = s;
+}
+
+// One pass's finalize as its own one-workgroup launch (eegnet_train_stage: synchronised-BatchNorm data
+// parallel).  The pass kernel ran with g.defer and left its sums in part2 row 0; the host all-reduced them.
+__global__ __launch_bounds__(512) void k_fin(Geo g, const float* prm, FinArgs fa, int pass, int ncols) {
+    extern __shared__ __attribute__((aligned(16))) double dfin[];
+    double* S = dfin + 2;
+    for (int c = threadIdx.x; c < ncols; c += blockDim.x) S[c] = fa.part2[c];
+    __syncthreads();
+    double* scr = dfin + tail_s_doubles(ncols);
+    switch (pass) {
+        case 0: fin1(g, prm, S, scr, fa); break;
+        case 1: fin2(g, S, fa); break;
+        case 2: fin3(g, prm, S, fa); break;
+        case 3: fin4(g, prm, S, fa); break;
+        default: fin5(g, prm, S, scr, fa); break;
+    }
 }
 
 // ================================================================================================

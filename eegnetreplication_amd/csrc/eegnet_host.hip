@@ -92,6 +92,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     memset(g, 0, sizeof(*g));
     g->trace = g_trace_buf;
     g->B = d->B; g->C = d->C; g->T = d->T; g->F1 = d->F1; g->D = d->D; g->K1 = d->K1;
+    g->Bn = d->B;
     g->F2 = d->F1 * d->D;
     if (g->B < 1) return fail(EEGNET_EINVAL, "B must be >= 1 (got %d)", g->B);
     if (g->K1 != 32 && g->K1 != 64) return fail(EEGNET_EINVAL, "K1 must be 32 or 64 (got %d)", g->K1);
@@ -331,11 +332,13 @@ static void ensure_attrs() {
     for (const void* f : {(const void*)k_wpass_b2<NTB2>, (const void*)k_wpass_c<NTB2>, (const void*)k_wpass_d<NTB2>,
                           (const void*)k_wpass_c<256>, (const void*)k_wpass_d<256>,
                           (const void*)k_wpass_c<256, true>, (const void*)k_wpass_d<256, true>,
-                          (const void*)k_coltail<3>, (const void*)k_coltail<4>, (const void*)k_coltail<5>})
+                          (const void*)k_coltail<3>, (const void*)k_coltail<4>, (const void*)k_coltail<5>,
+                          (const void*)k_fin})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
                           (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>,
-                          (const void*)k_infer_bf16<8, true>, (const void*)k_infer_bf16_cfg5})
+                          (const void*)k_infer_bf16<8, true>, (const void*)k_infer_bf16_cfg5,
+                          (const void*)k_infer_bf16_cfg5r})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 0, 0, 0>();
     set_attrs_shape<64, 0, 0, 0>();
@@ -435,7 +438,7 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
 template <int K1>
 static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
                        const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s,
-                       const FoldCall& fc = FoldCall{}, int nf = 1) {
+                       const FoldCall& fc = FoldCall{}, int nf = 1, int only = -1) {
     if (g.wide) return run_forward_wide<K1>(g, L, ws, params, bn, x, m2, update_running, nbt, s);
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
@@ -443,8 +446,8 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
                                                    g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc); \
     else hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsA * 4, s, \
                                                    g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc)
-    { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
-    } LAUNCH_CHECK("k_pass_a");
+    if (only < 0 || only == 0) { { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
+    } LAUNCH_CHECK("k_pass_a"); }
 #define LAUNCH_B(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
                        g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
                        (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
@@ -453,8 +456,8 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
                        g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
                        (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
                        (float*)(ws + L.partB), fb, fc)
-    { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
-    } LAUNCH_CHECK("k_pass_b");
+    if (only < 0 || only == 1) { { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
+    } LAUNCH_CHECK("k_pass_b"); }
     return 0;
 }
 
@@ -463,7 +466,8 @@ template <int K1>
 static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params,
                         const float* x, const uint8_t* m2, const uint8_t* m3, const float* dlogits,
                         const int64_t* labels, float* logits, float* grads, float* loss, int c_mode,
-                        const FinArgs* adam, hipStream_t s, const FoldCall& fc = FoldCall{}, int nf = 1) {
+                        const FinArgs* adam, hipStream_t s, const FoldCall& fc = FoldCall{}, int nf = 1,
+                        int only = -1) {
     if (g.wide)
         return run_backward_wide<K1>(g, L, ws, params, x, m2, m3, dlogits, labels, logits, grads, loss, c_mode,
                                      adam, s);
@@ -483,6 +487,7 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        g, params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits, \
                        (float*)(ws + L.dl), (float*)(ws + L.partC), c_mode, fcC, fc)
     if (use_b2_narrow(g)) {
+        if (only >= 0) return fail(EEGNET_EINVAL, "staged steps do not support EEGNET_B2=1");
         { PROF(KID_C);
           if (fc.folds) hipLaunchKernelGGL((k_wpass_c<256, true>), dim3(g.gridB2, nf), dim3(256), g.ldsWC * 4, s, g,
                                            params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits,
@@ -503,8 +508,8 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                                   (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, fc);
         } LAUNCH_CHECK("k_wpass_d<256>");
     } else {
-    { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
-    } LAUNCH_CHECK("k_pass_c(bwd)");
+    if (only < 0 || only == 2) { { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
+    } LAUNCH_CHECK("k_pass_c(bwd)"); }
 #define LAUNCH_D(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, true, false>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
@@ -520,8 +525,8 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
                        m2, m3, dl, (float*)(ws + L.dp2), \
                        (float*)(ws + L.partD), fd, fc)
-    { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
-    } LAUNCH_CHECK("k_pass_d");
+    if (only < 0 || only == 3) { { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
+    } LAUNCH_CHECK("k_pass_d"); }
     }
 #define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
                        g, (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v), \
@@ -529,8 +534,8 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     else hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
                        g, (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v), \
                        (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc)
-    { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
-    } LAUNCH_CHECK("k_pass_e");
+    if (only < 0 || only == 4) { { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
+    } LAUNCH_CHECK("k_pass_e"); }
     return 0;
 }
 
@@ -720,11 +725,13 @@ int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const
     const dim3 grid(std::min(g.B, device_cus())), blk(NTI);
     PROF(KID_INFER_BF16);
     if (same_geo_bf16(g, kGeoCfg5)) {
-        // time-chunked cfg5 kernel, two workgroups per CU (eegnet_infer_bf16c.hip); EEGNET_BF16_V1=1
-        // keeps the whole-trial kernel (A/B measurements)
-        static const bool v1 = getenv("EEGNET_BF16_V1") && getenv("EEGNET_BF16_V1")[0] == '1';
-        if (v1) hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
-        else hipLaunchKernelGGL(k_infer_bf16_cfg5, dim3(std::min(g.B, 2 * device_cus())), dim3(c5::NT), c5::LDS, s,
+        // time-chunked cfg5 kernel without an x halo, two workgroups per CU (eegnet_infer_bf16r.hip);
+        // EEGNET_BF16_KERNEL=w keeps the whole-trial kernel, =c the haloed chunk kernel (A/B measurements)
+        static const char kv = getenv("EEGNET_BF16_KERNEL") ? getenv("EEGNET_BF16_KERNEL")[0] : 'c';
+        if (kv == 'w') hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
+        else if (kv == 'c') hipLaunchKernelGGL(k_infer_bf16_cfg5, dim3(std::min(g.B, 2 * device_cus())), dim3(c5::NT),
+                                               c5::LDS, s, g, params, bn_buffers, x, logits);
+        else hipLaunchKernelGGL(k_infer_bf16_cfg5r, dim3(std::min(g.B, 2 * device_cus())), dim3(c5r::NT), c5r::LDS, s,
                                 g, params, bn_buffers, x, logits);
         LAUNCH_CHECK("k_infer_bf16(cfg5)");
         return 0;
@@ -791,6 +798,86 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     return g.K1 == 32
         ? run_backward<32>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, ap, s)
         : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, logits, grads, loss, mode, ap, s);
+}
+
+// One stage of a data-parallel train step with synchronised BatchNorm (distributed.py
+// DataParallelTrainer(sync_bn=True)): stage 2k launches pass k (A..E) with its finalize deferred --
+// the reduction's winner leaves the pass's fp64 sums at eegnet_stage_sums' place in the workspace for
+// the host to all-reduce over the ranks --, stage 2k + 1 runs pass k's finalize (k_fin) on the reduced
+// sums.  norm_batch: the global batch (BN statistics, the CE mean), so every finalize sees global-batch
+// sums and the gradients, running statistics, clamps and Adam come out identical on every rank.
+int eegnet_train_stage(const eegnet_dims* dims, int stage, int64_t norm_batch, float* params, float* bn_buffers,
+                       const float* x, const int64_t* labels, uint64_t seed, uint64_t offset, float* grads,
+                       float* adam_state, int32_t* step, float lr, float beta1, float beta2, float eps,
+                       float* loss, void* ws, void* stream, int flags, int64_t* num_batches_tracked) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (g.wide) return fail(EEGNET_EINVAL, "eegnet_train_stage: F1*D = %d > 16 is not supported", g.F2);
+    if (stage < 0 || stage >= 2 * TK_COUNT) return fail(EEGNET_EINVAL, "stage must be in [0, %d) (got %d)", 2 * TK_COUNT, stage);
+    if (norm_batch < g.B || norm_batch > (1LL << 30))
+        return fail(EEGNET_EINVAL, "norm_batch must be in [B, 2^30] (got %lld)", (long long)norm_batch);
+    if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
+    if (int r = check_ptrs(x, "x", labels, "labels")) return r;
+    if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
+    if (adam_state && !step) return fail(EEGNET_EINVAL, "step is NULL");
+    g.Bn = (int)norm_batch;
+    g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
+    g.drop = g.p > 0.f ? 1 : 0;
+    set_key(&g, seed, offset);
+    if (flags & EEGNET_KEY_FROM_STEP) {
+        if (!step) return fail(EEGNET_EINVAL, "EEGNET_KEY_FROM_STEP needs the device step counter");
+        g.keystep = step; g.kseed = seed; g.koff = offset;
+    }
+    ensure_attrs();
+    const WsLayout L = make_layout(g);
+    hipStream_t s = (hipStream_t)stream;
+    char* w = (char*)ws;
+    const int pass = stage >> 1;
+    FinArgs adam;
+    memset(&adam, 0, sizeof(adam));
+    adam.adam_m = adam_state; adam.adam_v = adam_state ? adam_state + g.nparam : nullptr; adam.step = step;
+    adam.lr = lr; adam.b1 = beta1; adam.b2 = beta2; adam.eps = eps;
+    if ((stage & 1) == 0) {
+        g.defer = 1;
+        if (pass < 2)
+            return g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s, FoldCall{}, 1, pass)
+                              : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s, FoldCall{}, 1, pass);
+        const int mode = PC_BWD | PC_CE;
+        return g.K1 == 32
+            ? run_backward<32>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, nullptr, grads, loss, mode, nullptr, s, FoldCall{}, 1, pass)
+            : run_backward<64>(g, L, w, params, x, nullptr, nullptr, nullptr, labels, nullptr, grads, loss, mode, nullptr, s, FoldCall{}, 1, pass);
+    }
+    FinArgs fa;
+    int ncols, lds;
+    switch (pass) {
+        case 0: fa = fin_args(L, w, TK_A, bn_buffers, nullptr, nullptr, 1, 0); ncols = g.nA; lds = g.ldsA; break;
+        case 1: fa = fin_args(L, w, TK_B, bn_buffers, nullptr, nullptr, 1, 0, num_batches_tracked); ncols = g.nB; lds = g.ldsB; break;
+        case 2: fa = fin_args(L, w, TK_C, nullptr, grads, loss, 0, 1); ncols = g.nC; lds = g.ldsC; break;
+        case 3: fa = fin_args(L, w, TK_D, nullptr, grads, nullptr, 0, 0); ncols = g.nD; lds = g.ldsD; break;
+        default:
+            fa = fin_args(L, w, TK_E, nullptr, grads, nullptr, 0, 0); ncols = g.nE; lds = g.ldsE;
+            if (adam_state) {
+                fa.params = params; fa.adam_m = adam.adam_m; fa.adam_v = adam.adam_v; fa.step = step;
+                fa.lr = lr; fa.b1 = beta1; fa.b2 = beta2; fa.eps = eps;
+            }
+            break;
+    }
+    hipLaunchKernelGGL(k_fin, dim3(1), dim3(NTB), (size_t)lds * 4, s, g, (const float*)params, fa, pass, ncols);
+    LAUNCH_CHECK("k_fin");
+    return 0;
+}
+
+// where stage 2k leaves pass k's sums in a workspace: byte offset and count of fp64 values
+int eegnet_stage_sums(const eegnet_dims* dims, int pass, size_t* offset_bytes, int* count) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (pass < 0 || pass >= TK_COUNT) return fail(EEGNET_EINVAL, "pass must be in [0, %d) (got %d)", TK_COUNT, pass);
+    if (!offset_bytes || !count) return fail(EEGNET_EINVAL, "null output pointer");
+    const WsLayout L = make_layout(g);
+    *offset_bytes = L.sums;
+    const int n[TK_COUNT] = {g.nA, g.nB, g.nC, g.nD, g.nE};
+    *count = n[pass];
+    return 0;
 }
 
 }  // extern "C"

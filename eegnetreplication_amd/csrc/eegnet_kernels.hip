@@ -41,4 +41,5 @@
 #include "eegnet_wide.hip"
 #include "eegnet_infer_bf16.hip"
 #include "eegnet_infer_bf16c.hip"
+#include "eegnet_infer_bf16r.hip"
 #include "eegnet_host.hip"

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
 #pragma unroll
     for (int j = 0; j < 2 * F2MAX; ++j) sdz[j] = 0.f;
     float bacc[NCLS] = {0.f, 0.f, 0.f, 0.f}, lossacc = 0.f;
-    const float invB = 1.0f / (float)g.B;
+    const float invB = 1.0f / (float)g.Bn;
 
     TRACE(g, 2, TR_PRO);
     TRACE_DECL();

@@ -658,7 +658,7 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
     for (int n = 0; n < NCLS; ++n) bfc[n] = prm[g.o_bfc + n];
     float sdz[4] = {0.f, 0.f, 0.f, 0.f}, sdzx[4] = {0.f, 0.f, 0.f, 0.f};
     float bacc[NCLS] = {0.f, 0.f, 0.f, 0.f}, lossacc = 0.f;
-    const float invB = 1.0f / (float)g.B;
+    const float invB = 1.0f / (float)g.Bn;
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {

@@ -70,13 +70,26 @@ class DataParallelTrainer:
     broadcast once at construction with the parameters: every rank then adds exactly one per step.
     The loss returned is the global-batch mean (the all-reduced per-rank means / world).
 
+    ``sync_bn=True`` (SURVEY 8(e)2's SyncBN option): BatchNorm normalises with GLOBAL-batch statistics.
+    The step is the single-device step of model.py:141-148 over the concatenated batch, split at its
+    five batch-global reductions (eegnet_train_stage): per pass, the HIP kernel leaves its fp64 sums in
+    the workspace, ONE all-reduce (SUM) of those sums runs (352 / 32 / 549 / 544 / 896 doubles for
+    EEGNet-8,2 at 22 x 256), and the pass's finalize runs on the global sums -- so BN statistics,
+    running statistics, the CE mean, the gradients, the clamps (on the global gradient) and the fused
+    Adam come out the same on every rank, with no separate gradient all-reduce and no buffer
+    broadcast.  Five latency-bound collectives per step instead of one; every rank's shard must have
+    the same size.
+
     The stages are methods so the orchestration can be exercised on CPU (gloo) with stand-ins for
     the device kernels.
     """
 
     def __init__(self, model: EEGNet, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, group=None,
-                 broadcast_buffers=True):
+                 broadcast_buffers=True, sync_bn=False):
         self.model = model
+        self.sync_bn = bool(sync_bn)
+        if self.sync_bn and model.shape.F2 > 16:
+            raise ValueError("sync_bn: F1*D > 16 is not supported (eegnet_train_stage)")
         self.lr, self.betas, self.eps = lr, betas, eps
         self.group = group
         self.broadcast_buffers = broadcast_buffers
@@ -158,7 +171,43 @@ class DataParallelTrainer:
         ops.adam_step(flat, grads, self.adam.state[:n], self.adam.state[n:], self.adam.step,
                       lr=self.lr, betas=self.betas, eps=self.eps)
 
+    # -- synchronised BatchNorm stages ----------------------------------------------------------
+    def stage(self, k, x, y, seed, offset):
+        """eegnet_train_stage k (2j: pass j with its sums left in the workspace; 2j + 1: its finalize)."""
+        m = self.model
+        B = x.shape[0]
+        ops.train_stage(m.shape, k, B * self.world, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed,
+                        offset, self.adam.grads, self.adam.state, self.adam.step, self.workspace(B),
+                        self.loss, lr=self.lr, betas=self.betas, eps=self.eps, nbt=m.flat_num_batches_tracked())
+
+    def stage_sums(self, B):
+        key = ("sums", B)
+        v = self._ws.get(key)
+        if v is None:
+            v = ops.stage_sums(self.model.shape, B, self.workspace(B))
+            self._ws[key] = v
+        return v
+
+    def reduce_sums(self, sums):
+        """ONE all-reduce (SUM) of a pass's fp64 sums."""
+        if self.world > 1:
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)
+        return sums
+
+    def step_sync_bn(self, x, y):
+        self._step += 1
+        seed = 0x5EED_0000 + self._step
+        offset = self._step * self.world + self.rank
+        sums = self.stage_sums(x.shape[0])
+        for j in range(5):
+            self.stage(2 * j, x, y, seed, offset)
+            self.reduce_sums(sums[j])
+            self.stage(2 * j + 1, x, y, seed, offset)
+        return self.loss
+
     def step(self, x, y):
+        if self.sync_bn:
+            return self.step_sync_bn(x, y)
         self._step += 1
         seed = 0x5EED_0000 + self._step
         offset = self._step * self.world + self.rank        # distinct masks on every rank

@@ -27,10 +27,11 @@ from .model import EEGNet, FusedAdamState
 
 
 class _FoldGraph:
-    """One fold's captured epoch: static permutation and per-step loss slots, and the graph."""
+    """One fold's captured epoch: the key it was captured under (every raw device pointer the graph
+    holds), static permutation and per-step loss slots, and the graph."""
 
-    def __init__(self, X, n, batch_size, perm, losses, graph):
-        self.X, self.n, self.batch_size = X, n, batch_size
+    def __init__(self, key, perm, losses, graph):
+        self.key = key
         self.perm, self.losses, self.graph = perm, losses, graph
 
 
@@ -89,6 +90,15 @@ class FoldBatch:
                            0, a.grads, a.state, a.step, self._workspace(k, xb.shape[0]),
                            losses[j:j + 1], lr=self.lr, betas=self.betas, eps=self.eps,
                            nbt=m.flat_num_batches_tracked(), key_from_step=True)
+
+    def _fold_key(self, k, X, y, batch_size):
+        """What fold k's captured epoch baked in: its model / Adam buffers (re-created by ``.to()``,
+        ``.float()`` or a re-flatten), its X and y, the batch size and workspace."""
+        m, a = self.models[k], self.adam[k]
+        return (X.shape[0], batch_size, id(X), X.data_ptr(), id(y), y.data_ptr(),
+                m.flat_parameters().data_ptr(), m.flat_bn_buffers().data_ptr(),
+                m.flat_num_batches_tracked().data_ptr(), a.state.data_ptr(), a.grads.data_ptr(),
+                a.step.data_ptr())
 
     # -- fused launches: all folds in one grid --------------------------------------------------
     def _fused_key(self, data, batch_size):
@@ -188,7 +198,8 @@ class FoldBatch:
             s.wait_stream(cur)
             st = self._graph[k]
             with torch.cuda.stream(s):
-                if st is not None and st.X is X and st.n == n and st.batch_size == batch_size:
+                key = self._fold_key(k, X, y, batch_size)
+                if st is not None and st.key == key:
                     st.perm.copy_(perm, non_blocking=True)
                     st.graph.replay()
                     sums.append(st.losses.sum(dtype=torch.float64))
@@ -203,7 +214,7 @@ class FoldBatch:
                     slosses = torch.zeros_like(losses)
                     with torch.cuda.graph(gr, stream=s):
                         self._steps(k, X, y, sperm, slosses, batch_size)
-                    self._graph[k] = _FoldGraph(X, n, batch_size, sperm, slosses, gr)
+                    self._graph[k] = _FoldGraph(key, sperm, slosses, gr)
         for s in self.streams:
             cur.wait_stream(s)
         for t in sums:

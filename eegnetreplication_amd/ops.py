@@ -184,6 +184,34 @@ def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset:
         "eegnet_train_step")
 
 
+def train_stage(shape: Shape, stage: int, norm_batch: int, flat_params, bn_flat, x, labels, seed: int,
+                offset: int, grads, adam_state, step_i32, ws, loss, lr=1e-3, betas=(0.9, 0.999), eps=1e-7,
+                p: float | None = None, nbt=None):
+    """eegnet_train_stage: stage 2k = pass k with its finalize deferred (sums left in ``ws``),
+    stage 2k + 1 = pass k's finalize on the (all-reduced) sums; statistics normalised by
+    ``norm_batch`` (the global batch of a synchronised-BatchNorm data-parallel step)."""
+    d = shape.dims(x.shape[0], p)
+    _lib.check(_lib.load().eegnet_train_stage(
+        ctypes.byref(d), ctypes.c_int(stage), ctypes.c_int64(norm_batch), _ptr(flat_params), _ptr(bn_flat),
+        _ptr(x), _ptr(labels), ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),
+        _ptr(step_i32), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
+        ctypes.c_float(eps), _ptr(loss), _ptr(ws), _stream(), 0, _ptr(nbt)), "eegnet_train_stage")
+
+
+def stage_sums(shape: Shape, B: int, ws: torch.Tensor, p: float | None = None) -> list[torch.Tensor]:
+    """The five float64 views of ``ws`` (a uint8 workspace tensor) that stages 0, 2, 4, 6, 8 leave
+    their sums in (one buffer, reused by every pass: view k holds pass k's sums after stage 2k)."""
+    d = shape.dims(B, p)
+    lib = _lib.load()
+    out = []
+    for k in range(5):
+        off, n = ctypes.c_size_t(0), ctypes.c_int(0)
+        _lib.check(lib.eegnet_stage_sums(ctypes.byref(d), ctypes.c_int(k), ctypes.byref(off), ctypes.byref(n)),
+                   "eegnet_stage_sums")
+        out.append(ws[off.value:off.value + 8 * n.value].view(torch.float64))
+    return out
+
+
 def fold_table(entries, device) -> torch.Tensor:
     """Device array of ``eegnet_fold`` entries (a uint8 tensor holding the packed structs).
     ``entries``: dicts with the eegnet_fold fields as tensors (or None) and ``seed`` as an int."""

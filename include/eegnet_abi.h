@@ -128,6 +128,26 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
                       float eps, float* loss, float* logits, void* ws, void* stream, int flags,
                       int64_t* num_batches_tracked);
 
+/* One stage of a data-parallel train step with synchronised BatchNorm (SURVEY 8(e)2's SyncBN option;
+ * the reference has no multi-device path -- this is the single-device semantics of model.py:141-148
+ * over the global batch, split at the five batch-global reductions so a caller can all-reduce each).
+ * stage 2k (k = 0..4: passes A..E) launches pass k and leaves its fp64 sums in the workspace
+ * (eegnet_stage_sums says where) instead of finalizing; stage 2k + 1 runs pass k's finalize on those
+ * sums once the caller has summed them over the ranks (all_reduce SUM).  norm_batch = the global batch:
+ * BatchNorm statistics, running statistics and the CE mean are normalised by it, so the gradients,
+ * clamps (model.py:44/84, on the global gradient) and the fused Adam of stage 9 come out the same on
+ * every rank and no separate gradient all-reduce is needed.  Other arguments as for eegnet_train_step
+ * (adam_state NULL: gradients only).  F1*D <= 16 only. */
+int eegnet_train_stage(const eegnet_dims* dims, int stage, int64_t norm_batch, float* params,
+                       float* bn_buffers, const float* x, const int64_t* labels, uint64_t seed,
+                       uint64_t offset, float* grads, float* adam_state, int32_t* step, float lr,
+                       float beta1, float beta2, float eps, float* loss, void* ws, void* stream,
+                       int flags, int64_t* num_batches_tracked);
+
+/* Where stage 2k leaves pass k's sums in a workspace of eegnet_workspace_bytes(dims): byte offset and
+ * number of fp64 values (the buffer a synchronised-BatchNorm caller all-reduces). */
+int eegnet_stage_sums(const eegnet_dims* dims, int pass, size_t* offset_bytes, int* count);
+
 /* One model (fold) of a fold-indexed train step: everything eegnet_train_step takes per model.
  * Every pointer is a device pointer; an array of these lives in DEVICE memory. */
 typedef struct eegnet_fold {

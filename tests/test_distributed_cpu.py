@@ -144,3 +144,57 @@ def test_lpt_assign_balances_and_is_deterministic():
     b = lpt_assign([10, 9, 8, 1, 1, 1], 2)
     loads = [sum([10, 9, 8, 1, 1, 1][i] for i in r) for r in b]
     assert max(loads) - min(loads) <= 4          # optimum for this instance is 13 | 17
+
+
+def _syncbn_worker(rank, world, port, q):
+    """DataParallelTrainer(sync_bn=True).step on CPU/gloo with stand-in device stages: stage 2j writes
+    a rank-specific fp64 sums vector for pass j, stage 2j + 1 records what the finalize sees."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from eegnetreplication_amd import EEGNet
+    from eegnetreplication_amd import distributed as D
+    D.init_process_group("gloo")
+    torch.manual_seed(7)
+    tr = D.DataParallelTrainer(EEGNet(22, 256, p=0.0), sync_bn=True)
+    sums = [torch.zeros(n, dtype=torch.float64) for n in (5, 2, 7, 3, 4)]
+    tr.stage_sums = lambda B: sums
+    seen = []
+
+    def stage(k, x, y, seed, offset):
+        j = k // 2
+        if k % 2 == 0:
+            sums[j].copy_(torch.arange(sums[j].numel(), dtype=torch.float64) * (rank + 1) + 100 * j)
+            seen.append(("pass", j, seed, offset))
+        else:
+            seen.append(("fin", j, sums[j].clone().numpy()))
+
+    tr.stage = stage
+    tr.step(torch.zeros(8, 22, 256), torch.zeros(8, dtype=torch.int64))
+    q.put((rank, seen))
+    dist.destroy_process_group()
+
+
+def test_sync_bn_step_reduces_every_pass_before_its_finalize():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_syncbn_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, seen in res:
+        assert [(e[0], e[1]) for e in seen] == [(s, j) for j in range(5) for s in ("pass", "fin")]
+        for e in seen:
+            if e[0] == "fin":                     # the finalize sees the sum over ranks of pass j's sums
+                j = e[1]
+                n = e[2].size
+                expect = sum(np.arange(n) * (r + 1) + 100 * j for r in range(world))
+                np.testing.assert_array_equal(e[2], expect)
+    # one seed, distinct dropout offsets per rank
+    p0 = [e for e in res[0][1] if e[0] == "pass"][0]
+    p1 = [e for e in res[1][1] if e[0] == "pass"][0]
+    assert p0[2] == p1[2] and p0[3] != p1[3]

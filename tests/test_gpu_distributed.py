@@ -210,3 +210,92 @@ def test_dp_trainer_world2_on_one_gpu():
         got[k] = res[0][1][o:o + p.numel()].reshape(p.shape)
         o += p.numel()
     assert_params_close(got, expect, prefix="DP world2 ")
+
+
+def test_sync_bn_world1_bit_identical_to_fused():
+    """DataParallelTrainer(sync_bn=True) at world_size 1: the staged step (each pass with its finalize
+    deferred, then k_fin on the sums) is the fused step split at its reductions -- bit-identical
+    parameters, BN buffers, counters, Adam state and losses to FusedTrainer over 3 steps."""
+    from eegnetreplication_amd import FusedTrainer
+    from eegnetreplication_amd.distributed import DataParallelTrainer
+    dev = _dev()
+    g = Golden("G1")
+    x = torch.from_numpy(g.x).to(dev)
+    y = torch.from_numpy(g.y).to(dev)
+    a, b = _model_from(g, dev), _model_from(g, dev)
+    dp, fu = DataParallelTrainer(a, sync_bn=True), FusedTrainer(b)
+    for s in range(3):
+        la = float(dp.step(x, y))
+        lb = float(fu.step(x, y))
+        assert la == lb, s
+    torch.cuda.synchronize()
+    assert torch.equal(a.flat_parameters(), b.flat_parameters())
+    assert torch.equal(a.flat_bn_buffers(), b.flat_bn_buffers())
+    assert torch.equal(dp.adam.state, fu.adam.state)
+    assert torch.equal(a.flat_num_batches_tracked(), b.flat_num_batches_tracked())
+
+
+def _syncbn_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import torch.distributed as dist
+    from eegnetreplication_amd import distributed as D
+    try:
+        D.init_process_group("gloo")
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        g = Golden("G6")
+        model = _model_from(g, dev)
+        tr = D.DataParallelTrainer(model, sync_bn=True)
+        half = g.x.shape[0] // world
+        x = torch.from_numpy(g.x[rank * half:(rank + 1) * half]).to(dev)
+        y = torch.from_numpy(g.y[rank * half:(rank + 1) * half]).to(dev)
+        losses = [float(tr.step(x, y))]
+        torch.cuda.synchronize()
+        q.put((rank, model.flat_parameters().cpu().numpy().copy(), losses, None,
+               model.flat_bn_buffers().cpu().numpy().copy(), tr.adam.state.cpu().numpy().copy()))
+        dist.destroy_process_group()
+    except Exception as e:                 # report instead of hanging the parent
+        q.put((rank, None, None, repr(e), None, None))
+        raise
+
+
+def test_sync_bn_world2_equals_single_device_on_the_whole_batch():
+    """Two ranks (gloo, both on cuda:0) with synchronised BatchNorm on the two halves of G6 take the
+    same step as ONE device on the whole batch (FusedTrainer): BN statistics over the global batch,
+    global CE mean, clamps on the global gradient, Adam -- running statistics, Adam moments and the
+    loss agree to fp32 summation order (rtol 1e-5), the parameters within assert_params_close (gamma1 /
+    beta1 take an O(lr) Adam step on rounding residue), and both ranks are identical."""
+    import torch.multiprocessing as mp
+    from eegnetreplication_amd import FusedTrainer
+    dev = _dev()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_syncbn_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[3] is None, f"rank {r[0]}: {r[3]}"
+    for p in procs:
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_array_equal(res[0][4], res[1][4])
+    np.testing.assert_array_equal(res[0][5], res[1][5])
+    assert res[0][2] == res[1][2]
+    g = Golden("G6")
+    m = _model_from(g, dev)
+    fu = FusedTrainer(m)
+    x, y = torch.from_numpy(g.x).to(dev), torch.from_numpy(g.y).to(dev)
+    ref_losses = [float(fu.step(x, y))]
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(res[0][2], ref_losses, rtol=1e-5)
+    assert_params_close(flat_to_dict(m, torch.from_numpy(res[0][1])), flat_to_dict(m, m.flat_parameters()),
+                        prefix="SyncBN world2 ")
+    for got, ref, what in ((res[0][4], m.flat_bn_buffers(), "bn"), (res[0][5], fu.adam.state, "adam")):
+        ref = ref.detach().cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6 * float(np.abs(ref).max()), err_msg=what)
