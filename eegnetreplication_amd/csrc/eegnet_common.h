@@ -57,6 +57,8 @@ struct Geo {
     int o_w1, o_g1, o_b1, o_ws, o_g2, o_b2, o_w2, o_W3, o_g3, o_b3, o_Wfc, o_bfc, nparam;
     // partial-row lengths of the five passes and the (common) workgroup count
     int nA, nB, nC, nD, nE;
+    int QR;              // rows of pass E's lag correlation Q in its partial row: F1 when every wave's
+                         // rows share one temporal group (narrow path, D = 2: summed before publishing), else F2
     int grid;            // workgroups of passes C, D and the eval forward
     int gridS;           // workgroups of the streaming passes A, B, E (two per CU)
     // LDS (floats)

@@ -69,6 +69,30 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     TRACE(g, tp, TR_PUB);
     if (!take_ticket(fa.cnt + grp, (unsigned)(r1 - r0), flag)) return false;
     TRACE_FS(g, tp, 0);            // last writer wins: about the last group
+    if (ngrp == 1) {
+        // one group (small grids: fold-indexed launches, small batches): its reducer IS the top level --
+        // the same sums in the same order as through part2 (0.0 + v == v), one round trip fewer
+        for (int c = tid; c < ncols; c += nth) {
+            const float* col = part + c;
+            double a = 0.0;
+            for (int rb = r0; rb < r1; rb += RGB) {
+                float v[RGB];
+#pragma unroll
+                for (int j = 0; j < RGB; ++j) v[j] = ld_pub(col + (size_t)min(rb + j, r1 - 1) * ncols);
+#pragma unroll
+                for (int j = 0; j < RGB; ++j) a += rb + j < r1 ? (double)v[j] : 0.0;
+            }
+            S[c] = a;
+        }
+        if (tid == 0) __hip_atomic_store(fa.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        TRACE(g, tp, TR_TOP);
+        if (g.defer) {
+            for (int c = tid; c < ncols; c += nth) fa.part2[c] = S[c];
+            return false;
+        }
+        return true;
+    }
     // group reducer: each thread sums whole columns, RGB row loads in flight, in row order
     for (int c = tid; c < ncols; c += nth) {
         const float* col = part + c;
@@ -350,7 +374,7 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     float* cf = (float*)(wd + F1 * K1);          // coefficient block [CF_COUNT][CSTR]
     float* gL = cf + CF_COUNT * CSTR;            // [0, o_g2): the gradients this finalize computes
     const double* Q = sums;
-    const double* Xm = sums + g.F2 * K1;
+    const double* Xm = sums + g.QR * K1;
     const double* Sdy = Xm + g.F2 * g.C;
     const double* Sdyv = Sdy + g.F2;
     // ---- one batch of global loads: statistics, taps, coefficients, Adam state ----
@@ -408,7 +432,8 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
         const int gg = p / K1, k = p - gg * K1;
         const double* w = wd + gg * K1;
         double qg = 0.0;
-        for (int o = gg * g.D; o < (gg + 1) * g.D; ++o) qg += Q[o * K1 + k];
+        if (g.QR == F1) qg = Q[gg * K1 + k];           // rows of a group summed in pass E
+        else for (int o = gg * g.D; o < (gg + 1) * g.D; ++o) qg += Q[o * K1 + k];
         double ux = 0.0;
         for (int l = 0; l < K1; ++l) ux += w[l] * Gm[l * K1 + k];
         const double inv1 = cf[CF_INV1 * CSTR + gg], mu1 = cf[CF_MU1 * CSTR + gg];

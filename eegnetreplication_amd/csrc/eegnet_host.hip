@@ -133,7 +133,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nB = 2 * g->F2;
     g->nC = NCLS * g->NF + NCLS + 2 * g->F2 + 1;
     g->nD = g->F2 * g->F2 + 18 * g->F2;
-    g->nE = g->F2 * g->K1 + g->F2 * g->C + 2 * g->F2;
+    g->QR = (g->F2 <= F2MAX && g->D == 2) ? g->F1 : g->F2;
+    g->nE = g->QR * g->K1 + g->F2 * g->C + 2 * g->F2;
     g->grid = std::min(g->B, device_cus() * grid_mult_cd());     // passes C, D, infer
     g->gridS = std::min(g->B, device_cus() * WGPC * grid_mult());     // streaming passes A, B, E
     const int rows1 = g->C * g->RS;                   // x rows (one buffer)

@@ -112,6 +112,18 @@ __device__ __forceinline__ void zero_fill(float* sm, int n, int C, int RS, int L
     }
 }
 
+// Zero only the pads [0, LP) and [LP + T, RS) of nrows LDS rows: the compile-time-shape passes DMA or
+// fully write every row's data window before its first read, so the prologue need not clear it (a
+// full clear of the x / s / dy rows was ~1.5 us of pass E's prologue, and it ran before the first
+// trial's loads were issued)
+__device__ __forceinline__ void zero_pads(float* sm, int nrows, int RS, int LP, int T, int tid) {
+    const int npad = RS - T;
+    for (int i = tid; i < nrows * npad; i += NTB) {
+        const int r = i / npad, k = i - r * npad;
+        sm[r * RS + (k < LP ? k : T + k)] = 0.f;
+    }
+}
+
 // LDS-DMA of n floats (n % 256 == 0, 16-byte aligned source) into a contiguous LDS array
 __device__ __forceinline__ void flat_dma(const float* __restrict__ src, int n, float* dst, int wave, int lane) {
     for (int i = wave; i < (n >> 8); i += NWB)
@@ -231,7 +243,15 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     int b0, b1;
     trial_range(g, b0, b1);
 
-    zero_fill<TT && (TT % 256 == 0)>(sm, (C + F2) * RS, C, RS, LP, T, tid);
+    constexpr bool XDMA = TT != 0;                    // compile-time shapes: x / s rows by LDS-DMA
+    // compile-time shapes: the first trial's x goes out by LDS-DMA before anything else; the pad fill,
+    // the weight loads and the edge decode below overlap it, and one barrier waits for all of it
+    if constexpr (XDMA) {
+        if (b0 < b1) x_dma_asm(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
+        zero_pads(sm, C + F2, RS, LP, T, tid);
+    } else {
+        zero_fill<false>(sm, (C + F2) * RS, C, RS, LP, T, tid);
+    }
     float aw[KS];
     load_ws_frag<KS>(prm + g.o_ws, C, F2, aw, lane);
     float tap[NTS][K1];
@@ -266,11 +286,9 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
             ea[i] = -2;                                  // unused slot
         }
     }
-    constexpr bool XDMA = TT != 0;                    // compile-time shapes: x / s rows by LDS-DMA
     float pf[XDMA ? 1 : PF];
     if constexpr (XDMA) {
-        if (b0 < b1) x_dma(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
-        __syncthreads();
+        barrier_vm<0>();                              // the first x landed, pads and tables written
     } else {
         if (b0 < b1) x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pf, tid);
         __syncthreads();
@@ -496,6 +514,14 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int b0, b1;
     trial_range(g, b0, b1);
+    const int NO = EEG_NO(TT);
+    constexpr int MO = EEG_MO(TT);
+    const int hr = fir_row(lane), oh = RPW * wave + hr;
+    // v of the next trial rides one trial ahead in registers (compile-time shapes); the first trial's
+    // is requested before anything else, so the table and coefficient loads below overlap it
+    constexpr bool VPF = TT != 0;
+    float vpf[MO][8];
+    if (VPF && b0 < b1) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
 
     for (int i = tid; i < 3 * F2 * RS2; i += NTB) sm[i] = 0.f;     // pads stay zero
     for (int i = tid; i < F2MAX * (K2 + F2MAX); i += NTB) {
@@ -507,23 +533,16 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         }
         Wt[i] = v;
     }
-    const int NO = EEG_NO(TT);
-    constexpr int MO = EEG_MO(TT);
     float sr[RPW], sr2[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) { sr[r] = 0.f; sr2[r] = 0.f; }
     // BN2 constants of this lane's FIR row (fir_row)
-    const int hr = fir_row(lane), oh = RPW * wave + hr;
     float alh, beh, gah, bth;
     {
         const int oo = oh < F2 ? oh : 0;
         alh = coef[CF_AL2 * CSTR + oo]; beh = coef[CF_BE2 * CSTR + oo];
         gah = prm[g.o_g2 + oo]; bth = prm[g.o_b2 + oo];
     }
-    // v of the next trial rides one trial ahead in registers (compile-time shapes)
-    constexpr bool VPF = TT != 0;
-    float vpf[MO][8];
-    if (VPF && b0 < b1) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
     __syncthreads();
 
     TRACE(g, 1, TR_PRO);
@@ -679,6 +698,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     }
     constexpr int NTS = FF ? 1 : RPW;
     const int D = FF ? 2 : g.D;
+    const int QR = FF ? FF / 2 : g.QR;           // Q rows in the partial row (EEGNet-8,2 shapes: F1)
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* const Ss = sm;                        // s rows
     float* const Dys = Ss + F2 * RS;             // dy2 rows, then (in place) e = FIR^T(dy2)
@@ -694,20 +714,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     static_assert(!XDMA || (CC && FF), "LDS-DMA staging is specialised to compile-time C and F2");
 
     TRACE_PS(g, 0);
-    zero_fill<XDMA>(sm, (2 * F2 + C) * RS, F2, RS, LP, T, tid);    // XDMA: the s data windows are the DMA's
+    if constexpr (!XDMA) zero_fill<false>(sm, (2 * F2 + C) * RS, F2, RS, LP, T, tid);
     TRACE_PS(g, 1);
     float tap[NTS][K1];
-    load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
-    TRACE_PS(g, 2);
-    // BN2 forward / backward constants per row, [F2][8] in LDS
-    float* CT = DP + ((F2 * T1 + 3) & ~3);
-    if (tid < 8 * F2) {
-        const int o = tid >> 3, f = tid & 7;
-        const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
-                         : f == 2 ? prm + g.o_g2 : f == 3 ? prm + g.o_b2 : f == 4 ? coef + CF_AO * CSTR
-                         : f == 5 ? coef + CF_BO * CSTR : coef + CF_CO * CSTR;
-        CT[tid] = src[o];
-    }
+    float* CT = DP + ((F2 * T1 + 3) & ~3);       // BN2 forward / backward constants per row, [F2][8]
     const int NO = EEG_NO(TT);
     constexpr int MO = EEG_MO(TT);
     const int hr = fir_row(lane), oh = RPW * wave + hr;
@@ -781,11 +791,14 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     float pdp[NDP];
     // specialised shapes: dp2 rows go straight to LDS by DMA (no registers, no exposed load)
     constexpr bool DPDMA = TT && FF && ((FF * (TT / 4)) % 256 == 0);
+    // compile-time shapes: the first trial's s / dp2 rows go out by LDS-DMA and its v into registers
+    // before anything else; the pad fill, the tap / coefficient loads overlap them and one barrier
+    // waits for all of it (in sequence these were four dependent round trips, ~6 us of prologue)
     if (b0 < b1) {
-        if constexpr (XDMA) x_dma(sg + (size_t)b0 * F2 * T, F2, T, RS, LP, Ss, wave, lane);
+        if constexpr (XDMA) x_dma_asm(sg + (size_t)b0 * F2 * T, F2, T, RS, LP, Ss, wave, lane);
         else s_rows_load(b0);
         TRACE_PS(g, 3);
-        if constexpr (DPDMA) flat_dma(dp2g + (size_t)b0 * ndp, ndp, DP, wave, lane);
+        if constexpr (DPDMA) flat_dma_asm(dp2g + (size_t)b0 * ndp, ndp, DP, wave, lane);
         else {
 #pragma unroll
             for (int j = 0; j < NDP; ++j) pdp[j] = dp2g[(size_t)b0 * ndp + min(tid + NTB * j, ndp - 1)];
@@ -797,7 +810,18 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         if constexpr (VPF) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
         TRACE_PS(g, 4);
     }
-    __syncthreads();
+    if constexpr (XDMA) zero_pads(sm, 2 * F2 + C, RS, LP, T, tid);   // the data windows are DMA'd / written
+    load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
+    TRACE_PS(g, 2);
+    if (tid < 8 * F2) {
+        const int o = tid >> 3, f = tid & 7;
+        const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
+                         : f == 2 ? prm + g.o_g2 : f == 3 ? prm + g.o_b2 : f == 4 ? coef + CF_AO * CSTR
+                         : f == 5 ? coef + CF_BO * CSTR : coef + CF_CO * CSTR;
+        CT[tid] = src[o];
+    }
+    if constexpr (XDMA) barrier_vm<0>();          // first s / dp2 landed (asm DMA), pads and tables written
+    else __syncthreads();
     if constexpr (!XDMA) {
         if (b0 < b1) {
             s_rows_put();
@@ -1094,15 +1118,18 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
 #pragma unroll
                 for (int j = 0; j < NH; ++j) {
                     const int idx = j + off;
-                    if (idx == 0) pub(row + (F2 * K1 + F2 * C + o), rv[j]);
-                    else if (idx == 1) pub(row + (F2 * K1 + F2 * C + F2 + o), rv[j]);
+                    if (idx == 0) pub(row + (QR * K1 + F2 * C + o), rv[j]);
+                    else if (idx == 1) pub(row + (QR * K1 + F2 * C + F2 + o), rv[j]);
                 }
             }
         }
     }
-    // Q: this wave's Cq tiles -> its own LDS slice [16 u][16 NWT w] (past the dws tiles) -> diagonal sums
+    // Q: this wave's Cq tiles -> its own LDS slice [16 u][16 NWT w] (past the dws tiles) -> diagonal
+    // sums; with D = 2 (QR = F1) the wave's two rows are one temporal group and publish their sum
     {
         float* CQ = red + NWB * 256 + wave * (256 * NWT);
+        const bool grp = QR != F2;
+        float qg = 0.f;                                // K1 <= 64: lane = lag k
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
             const int o = RPW * wave + r;
@@ -1112,15 +1139,17 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
 #pragma unroll
                     for (int q = 0; q < 4; ++q) CQ[(4 * lk + q) * (16 * NWT) + 16 * j + li] = cq[r][j][q];
                 wave_lds_fence();
-                for (int k = lane; k < K1; k += 64) {
+                if (lane < K1) {
                     float a = 0.f;
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) a += CQ[u * (16 * NWT) + u + k];
-                    pub(row + (o * K1 + k), a);
+                    for (int u = 0; u < 16; ++u) a += CQ[u * (16 * NWT) + u + lane];
+                    if (grp) qg += a;
+                    else pub(row + (o * K1 + lane), a);
                 }
                 wave_lds_fence();
             }
         }
+        if (grp && RPW * wave < F2 && lane < K1) pub(row + (wave * K1 + lane), qg);
     }
     // Xm: wave -> 16x16 tile partial (rows 4lk+q, col li) -> LDS [wave][256] -> sum over the
     // waves of each c-tile
@@ -1132,7 +1161,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         const int ct2 = c >> 4, cc = c & 15;
         float a = 0.f;
         for (int w = ct2 * wpc; w < (ct2 + 1) * wpc; ++w) a += red[w * 256 + oo2 * 16 + cc];
-        pub(row + (F2 * K1 + p), a);
+        pub(row + (QR * K1 + p), a);
     }
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nE, fa, dsm)) { fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa); TRACE(g, 4, TR_FIN); }
