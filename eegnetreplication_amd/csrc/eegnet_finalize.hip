@@ -53,6 +53,8 @@ __device__ __forceinline__ bool take_ticket(unsigned* w, unsigned target, int* f
 // longer in use once the partial row is written): [flag 2][S rup2(ncols)][scratch]
 __host__ __device__ constexpr int tail_scratch_doubles(int ncols) { return ncols > NTH ? ncols : NTH; }
 constexpr int RGB = 16;           // partial rows per group reducer batch (one round trip)
+constexpr int FLAT_PH = 16;       // row phases per column of a one-level reduction
+constexpr long long FLAT_ELEMS = 16384;   // partial-row elements (grid x ncols) reduced in one level
 __host__ __device__ constexpr int tail_s_doubles(int ncols) { return 2 + ((ncols + 1) & ~1); }
 
 __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const FinArgs& fa, double* dsm) {
@@ -62,13 +64,49 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     // partial rows per group / groups from this launch's own grid (passes use different grids):
     // groups of <= RGB rows, so a group reducer fetches each column's rows in one batch
     const int grid = gridDim.x;
-    const int rgs = max(RGB, (grid + NGRPMAX - 1) / NGRPMAX), ngrp = (grid + rgs - 1) / rgs;
+    // narrow partial rows (pass B's 32 columns): every row in ONE group, read by all threads at once
+    // (column x row phase), so the pass ends in one ticket and one batch of loads
+    const bool flat = (long long)grid * ncols <= FLAT_ELEMS && ncols * FLAT_PH <= nth;
+    const int rgs = flat ? grid : max(RGB, (grid + NGRPMAX - 1) / NGRPMAX), ngrp = (grid + rgs - 1) / rgs;
     const int grp = blockIdx.x / rgs;
     const int r0 = grp * rgs, r1 = min(grid, r0 + rgs);
     const int tp = fa.tpass;
     TRACE(g, tp, TR_PUB);
     if (!take_ticket(fa.cnt + grp, (unsigned)(r1 - r0), flag)) return false;
     TRACE_FS(g, tp, 0);            // last writer wins: about the last group
+    if (flat) {
+        // thread (column c, phase ph) sums rows ph, ph + FLAT_PH, ... in order; the phases are then
+        // combined in phase order (fixed by (row, column) alone: deterministic)
+        double* ph = S + ((ncols + 1) & ~1);           // [ncols][FLAT_PH] scratch after S
+        const int c = tid / FLAT_PH, q = tid - c * FLAT_PH;
+        if (c < ncols) {
+            const float* col = part + c;
+            double a = 0.0;
+            for (int rb = q; rb < grid; rb += RGB * FLAT_PH) {
+                float v[RGB];
+#pragma unroll
+                for (int j = 0; j < RGB; ++j) v[j] = ld_pub(col + (size_t)min(rb + j * FLAT_PH, grid - 1) * ncols);
+#pragma unroll
+                for (int j = 0; j < RGB; ++j) a += rb + j * FLAT_PH < grid ? (double)v[j] : 0.0;
+            }
+            ph[c * FLAT_PH + q] = a;
+        }
+        if (tid == 0) __hip_atomic_store(fa.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        for (int cc = tid; cc < ncols; cc += nth) {
+            double a = 0.0;
+#pragma unroll
+            for (int k = 0; k < FLAT_PH; ++k) a += ph[cc * FLAT_PH + k];
+            S[cc] = a;
+        }
+        __syncthreads();
+        TRACE(g, tp, TR_TOP);
+        if (g.defer) {
+            for (int cc = tid; cc < ncols; cc += nth) fa.part2[cc] = S[cc];
+            return false;
+        }
+        return true;
+    }
     if (ngrp == 1) {
         // one group (small grids: fold-indexed launches, small batches): its reducer IS the top level --
         // the same sums in the same order as through part2 (0.0 + v == v), one round trip fewer

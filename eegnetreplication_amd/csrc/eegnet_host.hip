@@ -338,8 +338,7 @@ static void ensure_attrs() {
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_infer_bf16<0>, (const void*)k_infer_bf16<1>, (const void*)k_infer_bf16<2>,
                           (const void*)k_infer_bf16<4>, (const void*)k_infer_bf16<8>, (const void*)k_infer_bf16<16>,
-                          (const void*)k_infer_bf16<8, true>, (const void*)k_infer_bf16_cfg5,
-                          (const void*)k_infer_bf16_cfg5r})
+                          (const void*)k_infer_bf16<8, true>, (const void*)k_infer_bf16_cfg5})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 0, 0, 0>();
     set_attrs_shape<64, 0, 0, 0>();
@@ -429,7 +428,8 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
                                       (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v),
                                       (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
     if (g.splitE) {
-        coltail(5, (const float*)(ws + L.partE), g.gridS, g.nE, fe, fin5_scratch_doubles(g.K1, g.F1, g.o_g2));
+        // one partial row per trial range (k_wpass_e's chunk workgroups share it, disjoint columns)
+        coltail(5, (const float*)(ws + L.partE), g.gridS / g.NOC, g.nE, fe, fin5_scratch_doubles(g.K1, g.F1, g.o_g2));
         LAUNCH_CHECK("k_coltail(E)");
     }
     return 0;
@@ -726,13 +726,11 @@ int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const
     const dim3 grid(std::min(g.B, device_cus())), blk(NTI);
     PROF(KID_INFER_BF16);
     if (same_geo_bf16(g, kGeoCfg5)) {
-        // time-chunked cfg5 kernel without an x halo, two workgroups per CU (eegnet_infer_bf16r.hip);
-        // EEGNET_BF16_KERNEL=w keeps the whole-trial kernel, =c the haloed chunk kernel (A/B measurements)
-        static const char kv = getenv("EEGNET_BF16_KERNEL") ? getenv("EEGNET_BF16_KERNEL")[0] : 'c';
-        if (kv == 'w') hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
-        else if (kv == 'c') hipLaunchKernelGGL(k_infer_bf16_cfg5, dim3(std::min(g.B, 2 * device_cus())), dim3(c5::NT),
-                                               c5::LDS, s, g, params, bn_buffers, x, logits);
-        else hipLaunchKernelGGL(k_infer_bf16_cfg5r, dim3(std::min(g.B, 2 * device_cus())), dim3(c5r::NT), c5r::LDS, s,
+        // time-chunked cfg5 kernel, two workgroups per CU (eegnet_infer_bf16c.hip); EEGNET_BF16_V1=1
+        // keeps the whole-trial kernel (A/B measurements)
+        static const bool v1 = getenv("EEGNET_BF16_V1") && getenv("EEGNET_BF16_V1")[0] == '1';
+        if (v1) hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
+        else hipLaunchKernelGGL(k_infer_bf16_cfg5, dim3(std::min(g.B, 2 * device_cus())), dim3(c5::NT), c5::LDS, s,
                                 g, params, bn_buffers, x, logits);
         LAUNCH_CHECK("k_infer_bf16(cfg5)");
         return 0;

@@ -41,5 +41,4 @@
 #include "eegnet_wide.hip"
 #include "eegnet_infer_bf16.hip"
 #include "eegnet_infer_bf16c.hip"
-#include "eegnet_infer_bf16r.hip"
 #include "eegnet_host.hip"

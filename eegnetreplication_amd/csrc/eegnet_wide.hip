@@ -47,10 +47,9 @@ __host__ __device__ constexpr int rb_stride(int T1) {
 
 // workgroup -> (o-chunk j, trial range [b0, b1)).  When the grid allows, the NOC chunk workgroups
 // of one trial range get blockIdx values equal mod 8 -- the same XCD -- so they share its L2 for x.
-__device__ __forceinline__ void wide_unit(const Geo& g, int& j, int& b0, int& b1) {
+__device__ __forceinline__ void wide_unit(const Geo& g, int& j, int& b0, int& b1, int& r) {
     const int G = gridDim.x, bi = blockIdx.x, NOC = g.NOC;
     const int nr = G / NOC;
-    int r;
     if (G % (8 * NOC) == 0) {
         const int xcd = bi & 7, slot = bi >> 3;
         j = slot % NOC;
@@ -61,6 +60,10 @@ __device__ __forceinline__ void wide_unit(const Geo& g, int& j, int& b0, int& b1
     }
     b0 = (int)((long long)r * g.B / nr);
     b1 = (int)((long long)(r + 1) * g.B / nr);
+}
+__device__ __forceinline__ void wide_unit(const Geo& g, int& j, int& b0, int& b1) {
+    int r;
+    wide_unit(g, j, b0, b1, r);
 }
 
 // s[i][t] = sum_c ws[o0 + i][c] x[c][t] for the 16 rows of one chunk (v_mfma_f32_16x16x4_f32).
@@ -155,7 +158,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
     const bool row_on = o < F2;
     float tap[K1];
 #pragma unroll
-    for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + ((row_on ? o : 0) / g.D) * K1 + k];
+    for (int k = 0; k < K1; ++k)       // wave-uniform: SGPRs (readfirstlane), not K1 VGPRs
+        tap[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prm[g.o_w1 + ((row_on ? o : 0) / g.D) * K1 + k])));
     const int NO = (T + 7) >> 3;
     float svl = 0.f, sv2l = 0.f, s0 = 0.f;
     // lag-Gram of this wave's slice channel on the matrix cores (the Hankel block product of pass E's
@@ -1044,8 +1048,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     constexpr int LP = G_::LP;
     const int C = g.C, T = g.T, F2 = g.F2, RS = g.RS, T1 = T >> 2, NT16 = (T + 15) >> 4;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    int j, b0, b1;
-    wide_unit(g, j, b0, b1);
+    int j, b0, b1, rr;
+    wide_unit(g, j, b0, b1, rr);
     const int o0 = 16 * j, nrows = min(16, F2 - o0);
     float* Ss = sm;
     float* Dys = Ss + 16 * RS;
@@ -1060,7 +1064,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
     const int oo = row_on ? o : 0;
     float tap[K1];
 #pragma unroll
-    for (int k = 0; k < K1; ++k) tap[k] = prm[g.o_w1 + (oo / g.D) * K1 + k];
+    for (int k = 0; k < K1; ++k)       // wave-uniform: SGPRs (readfirstlane), not K1 VGPRs
+        tap[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prm[g.o_w1 + (oo / g.D) * K1 + k])));
     if (tid < 8 * 16) {
         const int r = tid >> 3, f = tid & 7, orr = min(o0 + r, F2 - 1);
         const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
@@ -1248,8 +1253,34 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
         if (lane == 16) rsum[2 * wave + 1] = rv[0];
     }
     __syncthreads();
-    float* row = part + (size_t)blockIdx.x * g.nE;
     const int nQ = F2 * K1, nX = F2 * C;
+    if (g.splitE) {
+        // k_coltail reduces: the NOC chunk workgroups of trial range rr write the disjoint column
+        // segments of their rows o0 .. o0 + nrows into ONE partial row rr (the rest of a full-width row
+        // per workgroup was zeros: 4x the publish and column-reduction bytes at cfg5)
+        float* rowr = part + (size_t)rr * g.nE;
+        for (int p = tid; p < nrows * K1; p += NTW) {       // Q[o][k]
+            const int w = p / K1, k = p - w * K1;
+            const float* cw = CQ + w * 256 * NWT + k;
+            float v = 0.f;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v += cw[u * (16 * NWT + 1)];
+            pub(rowr + (o0 * K1 + p), v);
+        }
+        for (int p = tid; p < nrows * C; p += NTW) {        // Xm[o][c]
+            const int w = p / C, c = p - w * C;
+            const int ct2 = c >> 4, cc = c & 15;
+            float v = 0.f;
+            for (int ww = ct2 * wpc; ww < (ct2 + 1) * wpc; ++ww) v += red[ww * 256 + w * 16 + cc];
+            pub(rowr + (nQ + o0 * C + p), v);
+        }
+        if (tid < nrows) {                                  // Sdy, Sdyv
+            pub(rowr + (nQ + nX + o0 + tid), rsum[2 * tid]);
+            pub(rowr + (nQ + nX + F2 + o0 + tid), rsum[2 * tid + 1]);
+        }
+        return;
+    }
+    float* row = part + (size_t)blockIdx.x * g.nE;
     for (int p = tid; p < g.nE; p += NTW) {
         float v = 0.f;
         if (p < nQ) {                                       // Q[o][k]
@@ -1272,7 +1303,6 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
         pub(row + p, v);
     }
     double* dsm = (double*)sm;
-    if (g.splitE) return;                            // k_coltail reduces and finalizes
     if (grid_reduce(g, part, g.nE, fa, dsm)) fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa);
 }
 
