@@ -2,7 +2,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/fprof
-timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fprof/kt -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-infer --no-cfg5 > gpurun_out/fprof/kt.log 2>&1 || { echo KT_FAIL; tail -20 gpurun_out/fprof/kt.log; exit 1; }
+timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fprof/kt -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-infer --no-cfg5 --no-cfg4 > gpurun_out/fprof/kt.log 2>&1 || { echo KT_FAIL; tail -20 gpurun_out/fprof/kt.log; exit 1; }
 python3 - <<'PY'
 import csv, glob
 f = glob.glob("gpurun_out/fprof/kt/**/run_kernel_stats.csv", recursive=True)[0]
