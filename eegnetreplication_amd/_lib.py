@@ -21,7 +21,7 @@ _lib = None
 class Fold(ctypes.Structure):
     """Mirror of ``eegnet_fold`` (include/eegnet_abi.h): one model of a fold-indexed step."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("params", "bn_buffers", "num_batches_tracked", "x", "labels",
-                                              "grads", "adam_state", "step", "losses", "ws")] + \
+                                              "grads", "adam_state", "step", "losses", "ws", "perm")] + \
                [("seed", ctypes.c_uint64)]
 
 
@@ -65,6 +65,8 @@ _SIGS = {
     "eegnet_profile_collect": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp, ctypes.c_int, _vp]),
     "eegnet_trace_enable": (ctypes.c_int, [_vp]),
     "eegnet_trace_bytes": (ctypes.c_size_t, []),
+    "eegnet_dims_bytes": (ctypes.c_size_t, []),
+    "eegnet_fold_bytes": (ctypes.c_size_t, []),
     "eegnet_last_error": (ctypes.c_char_p, []),
     "eegnet_build_info": (ctypes.c_char_p, []),
 }
@@ -88,6 +90,10 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        for name, mirror in (("eegnet_dims_bytes", Dims), ("eegnet_fold_bytes", Fold)):
+            if getattr(lib, name)() != ctypes.sizeof(mirror):
+                raise RuntimeError(f"{p} was built with another {mirror.__name__} layout ({name}() = "
+                                   f"{getattr(lib, name)()}, binding {ctypes.sizeof(mirror)}): rebuild it")
         if path is None:
             _lib = lib
         return lib

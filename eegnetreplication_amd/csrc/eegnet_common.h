@@ -76,6 +76,33 @@ struct Geo {
     int defer;           // the reduction's winner leaves the pass's sums in part2 row 0; no finalize
 };
 
+// Compile-time cfg5 geometry (EEGNet-16,4 at 64ch x 512, K1 = 32): the shape fields make_geo computes
+// for those dims (everything but B, the grids and the run-time keys / pointers).  The host launches
+// the SPEC instantiations of the wide kernels only when the run-time geometry matches these field for
+// field (eegnet_host.hip same_shape_w5), so a specialisation cannot disagree with the generic path;
+// with the bounds, strides and offsets constant the kernels fold their index arithmetic and unroll
+// (the bf16 eval kernel's kGeoCfg5 does the same, eegnet_infer_bf16.hip).
+#define EEG_SHAPE_W5(X)                                                                             \
+    X(C, 64) X(T, 512) X(F1, 16) X(D, 4) X(F2, 64) X(K1, 32) X(P, 15) X(R, 16) X(T1, 128) X(T2, 16)  \
+    X(NF, 1024) X(LP, 16) X(RS, 548) X(TQ, 128) X(NT16, 32) X(RS2, 144) X(RSW, 156) X(CK, 64)       \
+    X(NCT, 4) X(NKG, 32) X(nH, 136) X(nTl, 120) X(nedge, 287) X(o_w1, 0) X(o_g1, 512) X(o_b1, 528)   \
+    X(o_ws, 544) X(o_g2, 4640) X(o_b2, 4704) X(o_w2, 4768) X(o_W3, 5792) X(o_g3, 9888) X(o_b3, 9952) \
+    X(o_Wfc, 10016) X(o_bfc, 14112) X(nparam, 14116) X(nA, 448) X(nB, 128) X(nC, 4229) X(nD, 5248)    \
+    X(nE, 6272) X(QR, 64) X(wide, 1) X(NOC, 4) X(CPC, 16) X(F2P, 64) X(RB, 144) X(splitC, 1)         \
+    X(splitD, 1) X(splitE, 1) X(ldsWA, 19120) X(ldsWB, 0) X(ldsWB2, 23872) X(ldsWC, 10528)           \
+    X(ldsWD, 37952) X(ldsWE, 21672) X(ldsWI, 37760)
+__host__ __device__ __forceinline__ void shape_w5(Geo& g) {
+#define EEG_SET_(f, v) g.f = v;
+    EEG_SHAPE_W5(EEG_SET_)
+#undef EEG_SET_
+}
+template <bool SPEC>
+__device__ __forceinline__ Geo geo_w(const Geo& gin) {
+    Geo g = gin;
+    if constexpr (SPEC) shape_w5(g);
+    return g;
+}
+
 // timeline stamps: wall clock (100 MHz) at kernel phase boundaries, shader-clock phase sums (loop)
 constexpr int TR_SLOTS = 16, TR_MAXWG = 2048;
 enum TraceEv { TR_ENTRY = 0, TR_PRO, TR_LOOP, TR_PUB, TR_GRP, TR_TOP, TR_FIN, TR_PH0 = 8 };
@@ -192,6 +219,25 @@ struct FoldCall {
     float lr, b1, b2, eps;        // Adam (pass E's finalize)
     WsOff off;
 };
+
+// this workgroup's record of a fold-indexed launch, read through the constant address space: the
+// pointers loaded from it are then known to be global (as kernel-argument pointers are), so the
+// accesses through them compile to global loads / stores instead of flat ones (a flat load also
+// counts against lgkmcnt, so every LDS wait would wait for the loads in flight too)
+__device__ __forceinline__ eegnet_fold fold_rec(const FoldCall& fc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(4))) eegnet_fold*)fc.folds)[blockIdx.y];
+#else
+    return fc.folds[blockIdx.y];                   // (the host pass of a device function)
+#endif
+}
+
+// batch row bb of a fold-indexed launch in the fold's epoch data: through the fold's epoch permutation
+// when it has one (FoldBatch keeps X / y unshuffled, so an epoch needs no gather of the trials), else
+// row row0 + bb.  Single-model launches pass perm = nullptr, row0 = 0: row bb.
+__device__ __forceinline__ long long fold_row(const int64_t* __restrict__ perm, long long row0, int bb) {
+    return perm ? perm[row0 + bb] : row0 + bb;
+}
 
 __device__ __forceinline__ FinArgs fold_fin(const FoldCall& fc, const eegnet_fold& f, int tk, int update_running,
                                             int ce, bool nbt, bool adam, int nparam) {

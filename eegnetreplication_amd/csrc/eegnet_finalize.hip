@@ -532,9 +532,10 @@ __global__ __launch_bounds__(512) void k_fin(Geo g, const float* prm, FinArgs fa
 // totals, and the last of them (ticket) stages the totals into LDS and runs the pass's finalize.
 // ================================================================================================
 constexpr int NTCT = 1024;        // threads of k_coltail: 64 columns x 16 row phases
-template <int FIN>
-__global__ __launch_bounds__(NTCT) void k_coltail(Geo g, const float* prm, const float* part, int nrows, int ncols,
+template <int FIN, bool SPEC = false>
+__global__ __launch_bounds__(NTCT) void k_coltail(Geo gin, const float* prm, const float* part, int nrows, int ncols,
                                                   FinArgs fa) {
+    const Geo g = geo_w<SPEC>(gin);
     extern __shared__ __attribute__((aligned(16))) double dsmt[];
     constexpr int NPH = NTCT / 64, NB8 = 16;               // row phases; loads in flight per thread
     const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;

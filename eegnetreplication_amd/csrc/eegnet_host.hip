@@ -330,6 +330,11 @@ static void ensure_attrs() {
     if (g_attr_done) return;
     set_attrs_wide<32>();
     set_attrs_wide<64>();
+    for (const void* f : {(const void*)k_wpass_a<32, true>, (const void*)k_wpass_b<32, true>, (const void*)k_wpass_e<32, true>,
+                          (const void*)k_winfer<32, true>, (const void*)k_wpass_b2<NTB2, true>,
+                          (const void*)k_wpass_c<NTB2, false, true>, (const void*)k_wpass_d<NTB2, false, true>,
+                          (const void*)k_coltail<3, true>, (const void*)k_coltail<4, true>, (const void*)k_coltail<5, true>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_wpass_b2<NTB2>, (const void*)k_wpass_c<NTB2>, (const void*)k_wpass_d<NTB2>,
                           (const void*)k_wpass_c<256>, (const void*)k_wpass_d<256>,
                           (const void*)k_wpass_c<256, true>, (const void*)k_wpass_d<256, true>,
@@ -373,21 +378,36 @@ static FinArgs fin_args(const WsLayout& L, char* ws, int tk, float* bn, float* g
 }
 
 
+// the run-time geometry has the compile-time cfg5 shape (eegnet_common.h EEG_SHAPE_W5): launch the
+// SPEC instantiations of the wide kernels
+static bool same_shape_w5(const Geo& g) {
+#define EEG_EQ_(f, v) && g.f == v
+    return true EEG_SHAPE_W5(EEG_EQ_);
+#undef EEG_EQ_
+}
+// one wide-kernel launch, SPEC (cfg5 shape, compile-time geometry) or generic
+#define WLAUNCH(sp, KG, KS, grid_, blk_, lds_, ...)                                               \
+    do {                                                                                          \
+        if (sp) hipLaunchKernelGGL(KS, grid_, blk_, lds_, __VA_ARGS__);                           \
+        else hipLaunchKernelGGL(KG, grid_, blk_, lds_, __VA_ARGS__);                              \
+    } while (0)
+
 // F2 > 16: passes A, B (no reduction), B2 (BN3 statistics)
 template <int K1>
 static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const float* params, float* bn,
                             const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s) {
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
-    { PROF(KID_WA); hipLaunchKernelGGL((k_wpass_a<K1>), dim3(g.gridS), dim3(NTW), g.ldsWA * 4, s, g, params, x,
-                                      (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa); }
+    const bool sp = K1 == 32 && same_shape_w5(g);
+    { PROF(KID_WA); WLAUNCH(sp, (k_wpass_a<K1>), (k_wpass_a<K1, K1 == 32>), dim3(g.gridS), dim3(NTW), g.ldsWA * 4, s, g,
+                            params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa); }
     LAUNCH_CHECK("k_wpass_a");
-    { PROF(KID_WB); hipLaunchKernelGGL((k_wpass_b<K1>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g, params,
-                                      (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2),
-                                      (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
-    { PROF(KID_WB2); hipLaunchKernelGGL(k_wpass_b2<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s, g, params,
-                                      (const float*)(ws + L.d2), (float*)(ws + L.q3), (float*)(ws + L.r3),
-                                      (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
+    { PROF(KID_WB); WLAUNCH(sp, (k_wpass_b<K1>), (k_wpass_b<K1, K1 == 32>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g,
+                            params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2),
+                            (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
+    { PROF(KID_WB2); WLAUNCH(sp, k_wpass_b2<NTB2>, (k_wpass_b2<NTB2, true>), dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s,
+                             g, params, (const float*)(ws + L.d2), (float*)(ws + L.q3), (float*)(ws + L.r3),
+                             (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
     return 0;
 }
 
@@ -405,28 +425,29 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;
         fe.lr = adam->lr; fe.b1 = adam->b1; fe.b2 = adam->b2; fe.eps = adam->eps;
     }
+    const bool sp = K1 == 32 && same_shape_w5(g);
     // the column-parallel reduction + finalize of a split pass (k_coltail, eegnet_finalize.hip)
     auto coltail = [&](int fin, const float* part, int nrows, int ncols, const FinArgs& fa, int scr) {
         const int nb = (ncols + 63) / 64;
         const size_t lds = 8 * (size_t)std::max(2 + (NTCT / 64) * 64, tail_s_doubles(ncols) + scr);
         PROF(KID_CTAIL);
-        if (fin == 3) hipLaunchKernelGGL(k_coltail<3>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
-        else if (fin == 4) hipLaunchKernelGGL(k_coltail<4>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
-        else hipLaunchKernelGGL(k_coltail<5>, dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
+        if (fin == 3) WLAUNCH(sp, k_coltail<3>, (k_coltail<3, true>), dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
+        else if (fin == 4) WLAUNCH(sp, k_coltail<4>, (k_coltail<4, true>), dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
+        else WLAUNCH(sp, k_coltail<5>, (k_coltail<5, true>), dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
     };
-    { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params, coef,
-                                      (const float*)(ws + L.r3), m3, dlogits, labels, logits, (float*)(ws + L.dl),
-                                      (float*)(ws + L.partC), c_mode, fc, FoldCall{}); } LAUNCH_CHECK("k_wpass_c(bwd)");
+    { PROF(KID_WC); WLAUNCH(sp, k_wpass_c<NTB2>, (k_wpass_c<NTB2, false, true>), dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s,
+                            g, params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits, (float*)(ws + L.dl),
+                            (float*)(ws + L.partC), c_mode, fc, FoldCall{}); } LAUNCH_CHECK("k_wpass_c(bwd)");
     if (g.splitC) { coltail(3, (const float*)(ws + L.partC), g.grid, g.nC, fc, 0); LAUNCH_CHECK("k_coltail(C)"); }
-    { PROF(KID_WD); hipLaunchKernelGGL(k_wpass_d<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s, g, params, coef,
-                                      (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
-                                      (const float*)(ws + L.q3), (const float*)(ws + L.r3), m2, m3, dl,
-                                      (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
+    { PROF(KID_WD); WLAUNCH(sp, k_wpass_d<NTB2>, (k_wpass_d<NTB2, false, true>), dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s,
+                            g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
+                            (const float*)(ws + L.q3), (const float*)(ws + L.r3), m2, m3, dl,
+                            (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
     LAUNCH_CHECK("k_wpass_d");
     if (g.splitD) { coltail(4, (const float*)(ws + L.partD), g.grid, g.nD, fd, 0); LAUNCH_CHECK("k_coltail(D)"); }
-    { PROF(KID_WE); hipLaunchKernelGGL((k_wpass_e<K1>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
-                                      (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v),
-                                      (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
+    { PROF(KID_WE); WLAUNCH(sp, (k_wpass_e<K1>), (k_wpass_e<K1, K1 == 32>), dim3(g.gridS), dim3(NTW), g.ldsWE * 4, s, g,
+                            (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v),
+                            (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe); } LAUNCH_CHECK("k_wpass_e");
     if (g.splitE) {
         // one partial row per trial range (k_wpass_e's chunk workgroups share it, disjoint columns)
         coltail(5, (const float*)(ws + L.partE), g.gridS / g.NOC, g.nE, fe, fin5_scratch_doubles(g.K1, g.F1, g.o_g2));
@@ -651,10 +672,11 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     FinArgs none;
     memset(&none, 0, sizeof(none));
     if (g.wide) {
-        { PROF(KID_WC); hipLaunchKernelGGL(k_wpass_c<NTB2>, dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s, g, params,
-                                          (const float*)(w + L.coef), (const float*)(w + L.r3), mask3,
-                                          (const float*)nullptr, (const int64_t*)nullptr, logits, (float*)nullptr,
-                                          (float*)nullptr, (int)PC_LOGITS, none, FoldCall{}); }
+        const bool sp = g.K1 == 32 && same_shape_w5(g);
+        { PROF(KID_WC); WLAUNCH(sp, k_wpass_c<NTB2>, (k_wpass_c<NTB2, false, true>), dim3(g.grid), dim3(NTB2),
+                                g.ldsWC * 4, s, g, params, (const float*)(w + L.coef), (const float*)(w + L.r3), mask3,
+                                (const float*)nullptr, (const int64_t*)nullptr, logits, (float*)nullptr,
+                                (float*)nullptr, (int)PC_LOGITS, none, FoldCall{}); }
         LAUNCH_CHECK("k_wpass_c(fwd)");
         return 0;
     }
@@ -700,7 +722,8 @@ int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const floa
     hipStream_t s = (hipStream_t)stream;
     if (g.wide) {
         PROF(KID_WINFER);
-        if (g.K1 == 32) hipLaunchKernelGGL(k_winfer<32>, dim3(g.grid), dim3(NTW), g.ldsWI * 4, s, g, params, bn_buffers, x, logits);
+        if (g.K1 == 32) WLAUNCH(same_shape_w5(g), k_winfer<32>, (k_winfer<32, true>), dim3(g.grid), dim3(NTW), g.ldsWI * 4, s,
+                                g, params, bn_buffers, x, logits);
         else hipLaunchKernelGGL(k_winfer<64>, dim3(g.grid), dim3(NTW), g.ldsWI * 4, s, g, params, bn_buffers, x, logits);
         LAUNCH_CHECK("k_winfer");
         return 0;
@@ -972,6 +995,9 @@ int eegnet_trace_enable(void* buf) {
     g_trace_buf = (unsigned long long*)buf;
     return 0;
 }
+
+size_t eegnet_dims_bytes(void) { return sizeof(eegnet_dims); }
+size_t eegnet_fold_bytes(void) { return sizeof(eegnet_fold); }
 
 size_t eegnet_trace_bytes(void) { return (size_t)8 * TR_MAXWG * TR_SLOTS * sizeof(unsigned long long); }
 

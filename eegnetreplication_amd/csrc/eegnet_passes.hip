@@ -154,14 +154,17 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     EEG_DIMS(g);
     TRACE(g, 2, TR_ENTRY);
     unsigned dk1;
+    const int64_t* perm = nullptr;                     // fold launches: labels through the permutation
+    long long row0 = 0;
     if (FOLD) {
-        const eegnet_fold& f = fc.folds[blockIdx.y];
+        const eegnet_fold f = fold_rec(fc);
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
         r3g = (const float*)(ws + fc.off.r3);
         mask3 = nullptr; dlin = nullptr; logits = nullptr;
-        labels = f.labels + fc.row0;
+        labels = f.labels;
+        perm = f.perm; row0 = fc.row0;
         dlout = (float*)(ws + fc.off.dl);
         part = (float*)(ws + fc.off.partC);
         fa = fold_fin(fc, f, TK_C, 0, 1, false, false, g.nparam);
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
 #pragma unroll
                 for (int n = 0; n < NCLS; ++n) se += expf(L[n] - mx);
                 const float lse = mx + logf(se);
-                const int y = (int)labels[b];
+                const int y = (int)labels[fold_row(perm, row0, b)];
                 const float Ly = y == 0 ? L[0] : y == 1 ? L[1] : y == 2 ? L[2] : L[3];
                 lossacc += lse - Ly;
 #pragma unroll
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
     TRACE(g, 3, TR_ENTRY);
     unsigned dk0, dk1;
     if (FOLD) {
-        const eegnet_fold& f = fc.folds[blockIdx.y];
+        const eegnet_fold f = fold_rec(fc);
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);

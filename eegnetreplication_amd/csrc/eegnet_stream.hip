@@ -218,10 +218,13 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 0, TR_ENTRY);
+    const int64_t* perm = nullptr;                 // fold launches: trial rows through the permutation
+    long long row0 = 0;
     if (FOLD) {                                    // fold-indexed launch: this fold's pointers
-        const eegnet_fold& f = fc.folds[blockIdx.y];
+        const eegnet_fold f = fold_rec(fc);
         prm = f.params;
-        x = f.x + fc.row0 * (long long)C * T;
+        x = f.x;
+        perm = f.perm; row0 = fc.row0;
         sg = (float*)((char*)f.ws + fc.off.s);
         vg = (float*)((char*)f.ws + fc.off.v);
         part = (float*)((char*)f.ws + fc.off.partA);
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     // compile-time shapes: the first trial's x goes out by LDS-DMA before anything else; the pad fill,
     // the weight loads and the edge decode below overlap it, and one barrier waits for all of it
     if constexpr (XDMA) {
-        if (b0 < b1) x_dma_asm(x + (size_t)b0 * C * T, C, T, RS, LP, Xb, wave, lane);
+        if (b0 < b1) x_dma_asm(x + fold_row(perm, row0, b0) * (C * T), C, T, RS, LP, Xb, wave, lane);
         zero_pads(sm, C + F2, RS, LP, T, tid);
     } else {
         zero_fill<false>(sm, (C + F2) * RS, C, RS, LP, T, tid);
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     if constexpr (XDMA) {
         barrier_vm<0>();                              // the first x landed, pads and tables written
     } else {
-        if (b0 < b1) x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pf, tid);
+        if (b0 < b1) x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * T), C, T, pf, tid);
         __syncthreads();
         x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         __syncthreads();
@@ -345,8 +348,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         barrier_lds();                                     // Ss complete, x read for good (LDS only:
                                                            // the previous trial's v stores stay in flight)
         if (bn < b1) {                                     // next x: lands by the closing barrier
-            if constexpr (XDMA) x_dma_asm(x + (size_t)bn * C * T, C, T, RS, LP, Xb, wave, lane);
-            else x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pf, tid);   // live over the FIR only
+            if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, bn) * (C * T), C, T, RS, LP, Xb, wave, lane);
+            else x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * T), C, T, pf, tid);   // live over the FIR only
         }
         TRACE_PH(g, 0, 1, tph_);
         // s rows -> the s plane [B][F2][T] (pass E's lag-correlation operand)
@@ -492,7 +495,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     TRACE(g, 1, TR_ENTRY);
     unsigned dk0;
     if (FOLD) {
-        const eegnet_fold& f = fc.folds[blockIdx.y];
+        const eegnet_fold f = fold_rec(fc);
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
@@ -684,12 +687,15 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 4, TR_ENTRY);
+    const int64_t* perm = nullptr;                 // fold launches: trial rows through the permutation
+    long long row0 = 0;
     if (FOLD) {
-        const eegnet_fold& f = fc.folds[blockIdx.y];
+        const eegnet_fold f = fold_rec(fc);
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
-        x = f.x + fc.row0 * (long long)C * T;
+        x = f.x;
+        perm = f.perm; row0 = fc.row0;
         sg = (const float*)(ws + fc.off.s);
         vg = (const float*)(ws + fc.off.v);
         dp2g = (const float*)(ws + fc.off.dp2);
@@ -825,7 +831,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     if constexpr (!XDMA) {
         if (b0 < b1) {
             s_rows_put();
-            x_prefetch<PF, NTB>(x + (size_t)b0 * C * T, C, T, pfx, tid);
+            x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * T), C, T, pfx, tid);
             x_store<PF, NTB>(pfx, C, T, RS, LP, Xb, tid);
         }
         __syncthreads();
@@ -892,7 +898,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         }
         // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
         // GEMM); they land during the lag correlation / FIR^T, by the next barrier
-        if constexpr (XDMA) x_dma_asm(x + (size_t)b * C * T, C, T, RS, LP, Xb, wave, lane);
+        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * T), C, T, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 2, tph_);
         {
             float tl[K1];
@@ -1044,7 +1050,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             if constexpr (XDMA) x_dma_asm(sg + (size_t)bn * F2 * T, F2, T, RS, LP, Ss, wave, lane);
             else {                                         // registers over the dws GEMM only
                 s_rows_load(bn);
-                x_prefetch<PF, NTB>(x + (size_t)bn * C * T, C, T, pfx, tid);
+                x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * T), C, T, pfx, tid);
             }
             if constexpr (DPDMA) flat_dma_asm(dp2g + (size_t)bn * ndp, ndp, DP, wave, lane);
             asm volatile("" ::: "memory");                 // the v loads issue after the DMA (barrier_vm)

@@ -130,11 +130,12 @@ __device__ __forceinline__ void stage_slice(const float* __restrict__ xs, int nc
 //   [G0 K1][S0][H nH][Tl nTl][hs R][ts P][Sv F2][Sv2 F2]
 // LDS: Gram slice rows [CPC][RS] | s rows [16][RS] | wave partials [NWW][K1 + 3]
 // ================================================================================================
-template <int K1>
-__global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict__ prm,
+template <int K1, bool SPEC = false>
+__global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restrict__ prm,
                                                  const float* __restrict__ x, float* __restrict__ sg,
                                                  float* __restrict__ vg, float* __restrict__ part,
                                                  FinArgs fa) {
+    const Geo g = geo_w<SPEC>(gin);
     using G_ = KG<K1>;
     constexpr int LP = G_::LP;
     constexpr int NEI = G_::template nei<NTW>();
@@ -311,11 +312,12 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo g, const float* __restrict_
 // this wave's row per lane, the next trial's loaded a trial ahead): no LDS, no barrier.  No
 // reduction (BN3's statistics are pass B2's).
 // ================================================================================================
-template <int K1>
-__global__ __launch_bounds__(NTW) void k_wpass_b(Geo g, const float* __restrict__ prm, const float* coef,
+template <int K1, bool SPEC = false>
+__global__ __launch_bounds__(NTW) void k_wpass_b(Geo gin, const float* __restrict__ prm, const float* coef,
                                                  const float* __restrict__ vg, const uint8_t* __restrict__ mask2,
                                                  float* __restrict__ d2g, float* __restrict__ E1g,
                                                  float* __restrict__ E2g) {
+    const Geo g = geo_w<SPEC>(gin);
     const int T = g.T, F2 = g.F2, T1 = T >> 2;
     const unsigned dk0 = drop_key(g, 0);
     int j, b0, b1;
@@ -520,10 +522,11 @@ constexpr int NTTW = 8;
 // C and D) and BN3 (model.py:71) batch statistics.  Partial row [Sr F2][Sr2 F2].
 // LDS: D2 [F2P][RB] | Q [F2P][RB] | W2s [F2P][16] | wave sums [NWB2][2][16]
 // ================================================================================================
-template <int NT>
-__global__ __launch_bounds__(NT) void k_wpass_b2(Geo g, const float* __restrict__ prm,
+template <int NT, bool SPEC = false>
+__global__ __launch_bounds__(NT) void k_wpass_b2(Geo gin, const float* __restrict__ prm,
                                                    const float* __restrict__ d2g, float* __restrict__ q3g,
                                                    float* __restrict__ r3g, float* __restrict__ part, FinArgs fa) {
+    const Geo g = geo_w<SPEC>(gin);
     const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, RB = g.RB, NJT = F2P >> 4;
     const int NT1 = (T1 + 15) >> 4;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -608,23 +611,27 @@ __device__ __forceinline__ void b2_bn3(const float* coef, const B2Map& mp, float
 // (PC_BWD) CE, classifier grads, BN3-bwd sums.  Partial row [dWfc 4*NF][dbfc 4][Sdz3 F2][Sdz3x F2][loss].
 // LDS: H [NF] (features, then their gradients) | class partials [(NT / 64)][4] | sums | XH [F2P][RB]
 // ================================================================================================
-template <int NT, bool FOLD = false>
-__global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__ prm, const float* coef,
+template <int NT, bool FOLD = false, bool SPEC = false>
+__global__ __launch_bounds__(NT) void k_wpass_c(Geo gin, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ r3g, const uint8_t* __restrict__ mask3,
                                                   const float* __restrict__ dlin, const int64_t* __restrict__ labels,
                                                   float* __restrict__ logits, float* __restrict__ dlout,
                                                   float* __restrict__ part, int mode, FinArgs fa, FoldCall fc) {
+    const Geo g = geo_w<SPEC>(gin);
     const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, T2 = g.T2, NF = g.NF, RB = g.RB;
     const int NJT = F2P >> 4, NT1 = (T1 + 15) >> 4;
     unsigned dk1;
+    const int64_t* perm = nullptr;                     // fold launches: labels through the permutation
+    long long row0 = 0;
     if (FOLD) {                                        // fold-indexed launch: this fold's pointers
-        const eegnet_fold& f = fc.folds[blockIdx.y];
+        const eegnet_fold f = fold_rec(fc);
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
         r3g = (const float*)(ws + fc.off.r3);
         mask3 = nullptr; dlin = nullptr; logits = nullptr;
-        labels = f.labels + fc.row0;
+        labels = f.labels;
+        perm = f.perm; row0 = fc.row0;
         dlout = (float*)(ws + fc.off.dl);
         part = (float*)(ws + fc.off.partC);
         fa = fold_fin(fc, f, TK_C, 0, 1, false, false, g.nparam);
@@ -724,7 +731,7 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
 #pragma unroll
                 for (int n = 0; n < NCLS; ++n) se += expf(L[n] - mx);
                 const float lse = mx + logf(se);
-                const int y = (int)labels[b];
+                const int y = (int)labels[fold_row(perm, row0, b)];
                 const float Ly = y == 0 ? L[0] : y == 1 ? L[1] : y == 2 ? L[2] : L[3];
                 if (tid == 0) lossacc += lse - Ly;
 #pragma unroll
@@ -811,19 +818,20 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo g, const float* __restrict__
 // [dW3 F2*F2][dw2 F2*16][Sdz2 F2][Sdz2x F2].
 // LDS: D2 [F2P][RB] | Q [F2P][RB] (q, then dq) | DR [F2P][RB] | W2s | Hd [NF] | item sums
 // ================================================================================================
-template <int NT, bool FOLD = false>
-__global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo g, const float* __restrict__ prm, const float* coef,
+template <int NT, bool FOLD = false, bool SPEC = false>
+__global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ d2g, const float* __restrict__ E1g,
                                                   const float* __restrict__ E2g, const float* __restrict__ q3g,
                                                   const float* __restrict__ r3g, const uint8_t* __restrict__ mask2,
                                                   const uint8_t* __restrict__ mask3, const float* __restrict__ dl,
                                                   float* __restrict__ dp2g, float* __restrict__ part, FinArgs fa,
                                                   FoldCall fc) {
+    const Geo g = geo_w<SPEC>(gin);
     const int F2 = g.F2, F2P = g.F2P, T1 = g.T1, T2 = g.T2, NF = g.NF, RB = g.RB;
     const int NJT = F2P >> 4, KS3 = F2P >> 2, NT1 = (T1 + 15) >> 4, TQ1 = (T1 + 3) >> 2;
     unsigned dk0, dk1;
     if (FOLD) {
-        const eegnet_fold& f = fc.folds[blockIdx.y];
+        const eegnet_fold f = fold_rec(fc);
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
@@ -1039,11 +1047,12 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo g, const float* __restric
 // Per trial and wave: v (loaded a trial ahead) -> dy2 | next dp2 row (DMA) | lag correlation |
 // FIR^T -> e over the dy row | next s row (DMA) | barrier | dws GEMM | barrier
 // ================================================================================================
-template <int K1>
-__global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const float* coef,
+template <int K1, bool SPEC = false>
+__global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, const float* coef,
                                                  const float* __restrict__ x, const float* __restrict__ sg,
                                                  const float* __restrict__ vg, const float* __restrict__ dp2g,
                                                  float* __restrict__ part, FinArgs fa) {
+    const Geo g = geo_w<SPEC>(gin);
     using G_ = KG<K1>;
     constexpr int LP = G_::LP;
     const int C = g.C, T = g.T, F2 = g.F2, RS = g.RS, T1 = T >> 2, NT16 = (T + 15) >> 4;
@@ -1312,9 +1321,10 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo g, const float* prm, const 
 // pointwise (MFMA), BN3 (running statistics), ELU, pool8 and the classifier.
 // LDS: s rows [16][RS] | D2 [F2P][RB] | Q [F2P][RB] | W2s [F2P][16] | H [NF] | affine [F2P][4]
 // ================================================================================================
-template <int K1>
-__global__ __launch_bounds__(NTW) void k_winfer(Geo g, const float* __restrict__ prm, const float* __restrict__ bn,
+template <int K1, bool SPEC = false>
+__global__ __launch_bounds__(NTW) void k_winfer(Geo gin, const float* __restrict__ prm, const float* __restrict__ bn,
                                                 const float* __restrict__ x, float* __restrict__ logits) {
+    const Geo g = geo_w<SPEC>(gin);
     using G_ = KG<K1>;
     constexpr int LP = G_::LP;
     const int C = g.C, T = g.T, F2 = g.F2, F2P = g.F2P, RS = g.RS, T1 = T >> 2, T2 = g.T2, NF = g.NF;

@@ -126,7 +126,6 @@ class FoldBatch:
         nsteps = (n + batch_size - 1) // batch_size
         # any change: new tables, and the graph (which baked the old pointers in) is dropped
         st = {"key": key, "src": [d for d in data], "graph": None,
-              "Xp": [torch.empty_like(X) for X, _ in data], "yp": [torch.empty_like(y) for _, y in data],
               "perm": [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(K)],
               "losses": [torch.zeros(nsteps, dtype=torch.float32, device=dev) for _ in range(K)],
               "tables": {}, "steps": []}
@@ -137,18 +136,17 @@ class FoldBatch:
                 ents = []
                 for k, m in enumerate(self.models):
                     a = self.adam[k]
+                    # x / labels stay unshuffled: the kernels read batch row r as row perm[r]
+                    X, y = data[k]
                     ents.append(dict(params=m.flat_parameters(), bn_buffers=m.flat_bn_buffers(),
-                                     num_batches_tracked=m.flat_num_batches_tracked(), x=st["Xp"][k],
-                                     labels=st["yp"][k], grads=a.grads, adam_state=a.state, step=a.step,
+                                     num_batches_tracked=m.flat_num_batches_tracked(), x=X, labels=y,
+                                     perm=st["perm"][k], grads=a.grads, adam_state=a.state, step=a.step,
                                      losses=st["losses"][k], ws=self._workspace(k, B), seed=self.seeds[k]))
                 st["tables"][B] = ops.fold_table(ents, dev)
         self._fz = st
         return st
 
     def _fused_steps(self, st, data):
-        for k, (X, y) in enumerate(data):
-            torch.index_select(X, 0, st["perm"][k], out=st["Xp"][k])
-            torch.index_select(y, 0, st["perm"][k], out=st["yp"][k])
         shape = self.models[0].shape
         K = len(self.models)
         for i, j, B in st["steps"]:

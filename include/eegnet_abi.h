@@ -161,6 +161,8 @@ typedef struct eegnet_fold {
     int32_t* step;                  /* Adam step counter (device int32)                           */
     float* losses;                  /* per-batch loss slots (NULL: not written)                   */
     void* ws;                       /* workspace of eegnet_workspace_bytes(dims), zeroed once     */
+    const int64_t* perm;            /* epoch permutation: batch row r is x / labels row perm[r]   */
+                                    /* (NULL: row r itself, i.e. x already shuffled)              */
     uint64_t seed;                  /* dropout key seed: key = mix(seed, offset + *step)          */
 } eegnet_fold;
 
@@ -169,8 +171,9 @@ typedef struct eegnet_fold {
  * each fold keeps its own parameters, BN buffers, Adam state, workspace and reductions.  Replaces
  * the per-fold loops of train.py:50-140 (within-subject, 36 runs) and train.py:182-290
  * (cross-subject, 90 runs) at batch 64 (train.py:87,229), where one model's step cannot fill the
- * GPU.  All folds train on batch [row0, row0 + dims.B) of their own x / labels; the loss goes to
- * losses[slot].  Dropout keys follow each fold's device step (EEGNET_KEY_FROM_STEP semantics with
+ * GPU.  All folds train on batch [row0, row0 + dims.B) of their own x / labels -- rows
+ * perm[row0 ...] of x / labels when the fold has a perm (the epoch's shuffle without a gather of
+ * the trials) -- and the loss goes to losses[slot].  Dropout keys follow each fold's device step (EEGNET_KEY_FROM_STEP semantics with
  * `offset`), so a captured graph draws fresh masks on every replay.  F1*D <= 16 only. */
 int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fold* folds, int64_t row0,
                             int64_t slot, uint64_t offset, float lr, float beta1, float beta2, float eps,
@@ -194,6 +197,12 @@ int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, 
  * finalize, shader-clock sums of in-loop phases).  NULL turns it off. */
 int eegnet_trace_enable(void* buf);
 size_t eegnet_trace_bytes(void);
+
+/* sizeof(eegnet_dims) and sizeof(eegnet_fold) as this library was compiled: a binding checks its
+ * struct mirrors against them at load (a stale library with another fold layout would read every
+ * fold after the first from the wrong offsets). */
+size_t eegnet_dims_bytes(void);
+size_t eegnet_fold_bytes(void);
 
 /* Thread-local description of the last error ("" if none). */
 const char* eegnet_last_error(void);

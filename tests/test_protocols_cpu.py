@@ -139,7 +139,8 @@ def test_device_loader_matches_dataloader_shuffle():
 def test_fold_batches_are_balanced(monkeypatch):
     """_run_units splits the units into balanced fold batches of at most fold_batch (90 at 48: 45 + 45, not 48 + 42),
     in unit order, and returns the results in unit order."""
-    from eegnetreplication_amd import train as T_
+    import importlib
+    T_ = importlib.import_module("eegnetreplication_amd.train")   # (the package exports train())
     seen = []
 
     def fake_run_folds(specs, epochs, device):
@@ -170,7 +171,8 @@ def test_failed_unit_is_retried_from_a_fresh_state(monkeypatch):
     once (one at a time), and one fold batch fails once (fold-batched); both runs complete with the
     results of a run without failures.  A device fault is not retried."""
     import pytest
-    from eegnetreplication_amd import train as T_
+    import importlib
+    T_ = importlib.import_module("eegnetreplication_amd.train")
     specs = [(None, None, list(range(10 + u)), [], None, 0.5, 100 + u) for u in range(5)]
     ref = [_fake_unit(sp) for sp in specs]
     calls = {"n": 0}
