@@ -220,6 +220,28 @@ struct FoldCall {
     WsOff off;
 };
 
+// Issue priority paced by progress through the workgroup's trial range.  Two workgroups share a CU in
+// passes A, B and E, and the wave arbiter favours the older one: the first-dispatched half of the
+// grid finished its trials in 32 µs and the second half in 53 µs (pass E, B = 4096, r3 stamps), so
+// each CU ran its last ~20 µs at one workgroup's occupancy.  A workgroup drops a priority level per
+// quarter of its range, so the one ahead yields to the one behind.
+#ifndef EEGNET_PRIO
+#define EEGNET_PRIO 1
+#endif
+__device__ __forceinline__ void pace_prio(int done, int total) {
+    if constexpr (EEGNET_PRIO != 0) {
+        switch ((done * 4) / total) {
+        case 0: __builtin_amdgcn_s_setprio(3); break;
+        case 1: __builtin_amdgcn_s_setprio(2); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
+        }
+    }
+}
+__device__ __forceinline__ void tail_prio() {       // publish / reduction / finalize: ahead of loops
+    if constexpr (EEGNET_PRIO != 0) __builtin_amdgcn_s_setprio(3);
+}
+
 // this workgroup's record of a fold-indexed launch, read through the constant address space: the
 // pointers loaded from it are then known to be global (as kernel-argument pointers are), so the
 // accesses through them compile to global loads / stores instead of flat ones (a flat load also

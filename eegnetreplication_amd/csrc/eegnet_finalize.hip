@@ -55,6 +55,11 @@ __host__ __device__ constexpr int tail_scratch_doubles(int ncols) { return ncols
 constexpr int RGB = 16;           // partial rows per group reducer batch (one round trip)
 constexpr int FLAT_PH = 16;       // row phases per column of a one-level reduction
 constexpr long long FLAT_ELEMS = 16384;   // partial-row elements (grid x ncols) reduced in one level
+// (and grids of at most 128 rows: 512 workgroups on one ticket word serialise their atomics -- pass B
+// at B = 4096 took 11.6 µs from the last publish to its end, 7.3 through two levels)
+#ifndef EEGNET_FLAT_MAXGRID
+#define EEGNET_FLAT_MAXGRID 128
+#endif
 __host__ __device__ constexpr int tail_s_doubles(int ncols) { return 2 + ((ncols + 1) & ~1); }
 
 __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const FinArgs& fa, double* dsm) {
@@ -66,7 +71,7 @@ __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const Fi
     const int grid = gridDim.x;
     // narrow partial rows (pass B's 32 columns): every row in ONE group, read by all threads at once
     // (column x row phase), so the pass ends in one ticket and one batch of loads
-    const bool flat = (long long)grid * ncols <= FLAT_ELEMS && ncols * FLAT_PH <= nth;
+    const bool flat = (long long)grid * ncols <= FLAT_ELEMS && ncols * FLAT_PH <= nth && grid <= EEGNET_FLAT_MAXGRID;
     const int rgs = flat ? grid : max(RGB, (grid + NGRPMAX - 1) / NGRPMAX), ngrp = (grid + rgs - 1) / rgs;
     const int grp = blockIdx.x / rgs;
     const int r0 = grp * rgs, r1 = min(grid, r0 + rgs);
@@ -400,9 +405,46 @@ __device__ __forceinline__ void adam_elem(float* p, float g, float* m, float* v,
     *p = *p - step_size * (mi / denom);
 }
 
+// Adam step size and sqrt(bias correction 2) of step s (torch/optim/adam.py single-tensor path)
+__device__ __forceinline__ void adam_scalars(const FinArgs& fa, int s, float& step_size, float& bc2s) {
+    step_size = (float)((double)fa.lr / (1.0 - pow((double)fa.b1, (double)s)));
+    bc2s = (float)sqrt(1.0 - pow((double)fa.b2, (double)s));
+}
+
+// The parameters pass E never reads -- [o_w2, nparam): block-2 depthwise and pointwise weights, BN3,
+// the classifier -- have their final gradients after pass D (fin3, fin4).  Pass E's workgroups take
+// their Adam update, a slice each: the narrow pass E's workgroups once they have lost the reduction
+// ticket (while the winner reduces; the winner's own slice rides in fin5's staged batch), the wide
+// pass E's in its prologue.  fin5 then updates [0, o_w2).  The same element update with the same
+// step: bit-identical.  Not for a deferred (synchronised-BN) pass, whose k_fin runs the whole update.
+__device__ __forceinline__ bool adam_early(const Geo& g, const FinArgs& fa) {
+    return fa.adam_m != nullptr && !g.defer;
+}
+__device__ __forceinline__ void adam_slice_range(const Geo& g, int part, int nparts, int& i0, int& i1) {
+    const int lo = g.o_w2, per = (g.nparam - lo + nparts - 1) / nparts;
+    i0 = min(g.nparam, lo + part * per);
+    i1 = min(g.nparam, i0 + per);
+}
+__device__ void adam_slice(const Geo& g, const FinArgs& fa, int part, int nparts) {
+    if (!adam_early(g, fa)) return;
+    int i0, i1;
+    adam_slice_range(g, part, nparts, i0, i1);
+    const int i = i0 + (int)threadIdx.x;
+    if (i0 + (int)(threadIdx.x & ~63u) >= i1) return;    // waves without an element (wave-uniform)
+    float step_size, bc2s;
+    adam_scalars(fa, *fa.step + 1, step_size, bc2s);   // *fa.step: fin5 of this pass advances it later
+    for (int k = i; k < i1; k += (int)blockDim.x) {
+        float pp = fa.params[k], mm = fa.adam_m[k], vv = fa.adam_v[k];
+        adam_elem(&pp, fa.grads[k], &mm, &vv, fa.b1, fa.b2, step_size, bc2s, fa.eps);
+        fa.params[k] = pp; fa.adam_m[k] = mm; fa.adam_v[k] = vv;
+    }
+}
+
 // after pass E: spatial grad (+ clamp, model.py:44), BN1 grads, temporal-conv grad; then Adam
 constexpr int APT = 8;            // Adam elements per finalize thread: nparam <= APT * blockDim
-__device__ void fin5(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
+// own_slice >= 0: this workgroup's adam_slice (of gridDim.x) joins the staged Adam elements
+__device__ void fin5(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa,
+                     int own_slice = -1) {
     const int tid = threadIdx.x, nth = blockDim.x, K1 = g.K1, F1 = g.F1;
     double* Gm = scr;                 // K1*K1 (+ S1 K1), from fa.stats
     double* S1 = Gm + K1 * K1;
@@ -417,6 +459,12 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     const double* Sdyv = Sdy + g.F2;
     // ---- one batch of global loads: statistics, taps, coefficients, Adam state ----
     const bool adam = fa.adam_m != nullptr;
+    const bool early = adam_early(g, fa);
+    const int na = early ? g.o_w2 : g.nparam;     // [o_w2, nparam): pass E's workgroups (adam_slice)
+    int si0 = 0, si1 = 0;                         // + this workgroup's own slice, as elements na ...
+    if (early && own_slice >= 0) adam_slice_range(g, own_slice, gridDim.x, si0, si1);
+    const int ne = na + (si1 - si0);
+    auto pidx = [&](int e) { return e < na ? e : si0 + (e - na); };
     float ap[APT], am[APT], av[APT], ag[APT];
     int step0;
     {
@@ -427,10 +475,10 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
         s1.load(prm + g.o_w1, F1 * K1);
         s2.load(fa.coef, CF_COUNT * CSTR);
         if (adam) {   // parameters, moments and the earlier finalizes' gradients (indices >= o_g2)
-            const int last = g.nparam - 1;
+            const int last = ne - 1;
 #pragma unroll
             for (int j = 0; j < APT; ++j) {
-                const int i = min(tid + nth * j, last);
+                const int i = pidx(min(tid + nth * j, last));
                 ap[j] = fa.params[i]; am[j] = fa.adam_m[i]; av[j] = fa.adam_v[i]; ag[j] = fa.grads[i];
             }
         }
@@ -485,19 +533,21 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     __syncthreads();                  // gL complete
     TRACE_FS(g, fa.tpass, 6);
     const int s = step0 + 1;
-    const float step_size = (float)((double)fa.lr / (1.0 - pow((double)fa.b1, (double)s)));
-    const float bc2s = (float)sqrt(1.0 - pow((double)fa.b2, (double)s));
+    float step_size, bc2s;
+    adam_scalars(fa, s, step_size, bc2s);
 #pragma unroll
     for (int j = 0; j < APT; ++j) {
-        const int i = tid + nth * j;
-        if (i < g.nparam) {
+        const int e = tid + nth * j;
+        if (e < ne) {
+            const int i = pidx(e);
             const float gr = i < g.o_g2 ? gL[i] : ag[j];
             adam_elem(&ap[j], gr, &am[j], &av[j], fa.b1, fa.b2, step_size, bc2s, fa.eps);
             fa.params[i] = ap[j]; fa.adam_m[i] = am[j]; fa.adam_v[i] = av[j];
         }
     }
     // parameters beyond the staged block (large models, e.g. EEGNet-16,4 at 64 x 512: 14,116)
-    for (int i = tid + nth * APT; i < g.nparam; i += nth) {
+    for (int e = tid + nth * APT; e < ne; e += nth) {
+        const int i = pidx(e);
         float pp = fa.params[i], mm = fa.adam_m[i], vv = fa.adam_v[i];
         const float gr = i < g.o_g2 ? gL[i] : fa.grads[i];
         adam_elem(&pp, gr, &mm, &vv, fa.b1, fa.b2, step_size, bc2s, fa.eps);

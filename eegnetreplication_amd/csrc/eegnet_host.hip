@@ -859,8 +859,8 @@ int eegnet_train_stage(const eegnet_dims* dims, int stage, int64_t norm_batch, f
     memset(&adam, 0, sizeof(adam));
     adam.adam_m = adam_state; adam.adam_v = adam_state ? adam_state + g.nparam : nullptr; adam.step = step;
     adam.lr = lr; adam.b1 = beta1; adam.b2 = beta2; adam.eps = eps;
+    g.defer = 1;                  // (k_fin: fin5 runs the whole Adam update, adam_early is off)
     if ((stage & 1) == 0) {
-        g.defer = 1;
         if (pass < 2)
             return g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s, FoldCall{}, 1, pass)
                               : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s, FoldCall{}, 1, pass);

@@ -304,6 +304,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
+        pace_prio(b - b0, b1 - b0);
         spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
         // lag-Gram: items (c, quad), lanes of a wave on consecutive quads of one row
         for (int j = tid; j < C * TQ; j += NTB) {
@@ -430,6 +431,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         TRACE_PH(g, 0, 4, tph_);
     }
     TRACE_LOOP(g, 0);
+    tail_prio();
 
     // ---- workgroup reduction -> one partial row ----
     float* row = part + (size_t)blockIdx.x * g.nA;
@@ -553,6 +555,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
+        pace_prio(b - b0, b1 - b0);
         float* Qs = Qs0 + ((b - b0) & 1) * F2 * RS2;
         float vc[MO][8];
         if constexpr (VPF) {
@@ -655,6 +658,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
         TRACE_PH(g, 1, 5, tph_);
     }
     TRACE_LOOP(g, 1);
+    tail_prio();
     {
         float rv[4] = {sr[0], sr[1], sr2[0], sr2[1]};
         wave_reduce<4>(rv);                        // lane 16k: item k = (k < 2 ? sr : sr2)[k % 2]
@@ -842,6 +846,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
+        pace_prio(b - b0, b1 - b0);
         float vc[MO][8];
         if constexpr (VPF) {
 #pragma unroll
@@ -1101,6 +1106,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         TRACE_PH(g, 4, 7, tph_);
     }
     TRACE_LOOP(g, 4);
+    tail_prio();
     __syncthreads();
 
     // ---- reductions ----
@@ -1170,7 +1176,12 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         pub(row + (QR * K1 + p), a);
     }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nE, fa, dsm)) { fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa); TRACE(g, 4, TR_FIN); }
+    if (grid_reduce(g, part, g.nE, fa, dsm)) {
+        fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa, blockIdx.x);
+        TRACE(g, 4, TR_FIN);
+    } else {
+        adam_slice(g, fa, blockIdx.x, gridDim.x);  // off the critical path: the winner is still reducing
+    }
 }
 
 }  // namespace eeg

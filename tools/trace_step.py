@@ -70,7 +70,7 @@ def main():
         if len(grp):
             line += f" | grp-red {(grp.max()-pub.max())/100:5.1f}"
         if len(top):
-            line += f" | top {(top.max()-grp.max())/100:5.1f}"
+            line += f" | top {(top.max()-(grp.max() if len(grp) else pub.max()))/100:5.1f}"
         if len(fin):
             line += f" | fin {(fin.max()-top.max())/100:5.1f}"
         line += f" | end {us(end):7.1f}"
