@@ -66,6 +66,7 @@ _SIGS = {
     "eegnet_trace_enable": (ctypes.c_int, [_vp]),
     "eegnet_trace_bytes": (ctypes.c_size_t, []),
     "eegnet_dims_bytes": (ctypes.c_size_t, []),
+    "eegnet_wide_spec": (ctypes.c_int, [ctypes.POINTER(Dims)]),
     "eegnet_fold_bytes": (ctypes.c_size_t, []),
     "eegnet_last_error": (ctypes.c_char_p, []),
     "eegnet_build_info": (ctypes.c_char_p, []),

@@ -90,7 +90,7 @@ struct Geo {
     X(o_Wfc, 10016) X(o_bfc, 14112) X(nparam, 14116) X(nA, 448) X(nB, 128) X(nC, 4229) X(nD, 5248)    \
     X(nE, 6272) X(QR, 64) X(wide, 1) X(NOC, 4) X(CPC, 16) X(F2P, 64) X(RB, 144) X(splitC, 1)         \
     X(splitD, 1) X(splitE, 1) X(ldsWA, 19120) X(ldsWB, 0) X(ldsWB2, 23872) X(ldsWC, 10528)           \
-    X(ldsWD, 37952) X(ldsWE, 21672) X(ldsWI, 37760)
+    X(ldsWD, 37952) X(ldsWE, 21736) X(ldsWI, 37760)
 __host__ __device__ __forceinline__ void shape_w5(Geo& g) {
 #define EEG_SET_(f, v) g.f = v;
     EEG_SHAPE_W5(EEG_SET_)
@@ -171,7 +171,7 @@ constexpr int TR_FINE = 6;
 // coefficient block layout (float, CSTR per field; F1, F2 <= 64)
 enum CoefField {
     CF_A1 = 0, CF_C1, CF_INV1, CF_MU1, CF_AL2, CF_BE2, CF_INV2, CF_MU3, CF_INV3,
-    CF_A3, CF_B3, CF_C3, CF_AO, CF_BO, CF_CO, CF_W, CF_LOSS, CF_COUNT
+    CF_A3, CF_B3, CF_C3, CF_AO, CF_BO, CF_CO, CF_W, CF_LOSS, CF_ADAM, CF_COUNT
 };
 constexpr int CSTR = 64;
 
@@ -181,7 +181,10 @@ enum PassCMode { PC_LOGITS = 1, PC_BWD = 2, PC_CE = 4 };
 // two-level fp64 reduction of its per-workgroup partial rows; the last workgroup to arrive runs that
 // pass's finalize.  Ticket words: NCNT per pass, zeroed by a memset node at the start of every call.
 constexpr int KSMAX = 16;       // ws MFMA k-steps: ceil(C / 4), C <= 64
-constexpr int NGRPMAX = 32;      // groups <= NCNT - 1 (ticket words)
+#ifndef EEGNET_NGRPMAX
+#define EEGNET_NGRPMAX 16
+#endif
+constexpr int NGRPMAX = EEGNET_NGRPMAX;   // groups <= NCNT - 1 (ticket words)
 constexpr int NCNT = 40;
 constexpr int SPLIT_COLS = 2048;  // wide passes with more partial-row columns reduce in k_coltail          // [0, ngrp) group tickets, [NCNT-1] the top-level ticket
 constexpr int TK_PASSES = 5;      // ticket blocks: passes A..E, contiguous from pass A's

@@ -52,7 +52,13 @@ __device__ __forceinline__ bool take_ticket(unsigned* w, unsigned target, int* f
 // LDS carve-up of the tail (doubles, from the start of the pass kernel's dynamic LDS, which is no
 // longer in use once the partial row is written): [flag 2][S rup2(ncols)][scratch]
 __host__ __device__ constexpr int tail_scratch_doubles(int ncols) { return ncols > NTH ? ncols : NTH; }
-constexpr int RGB = 16;           // partial rows per group reducer batch (one round trip)
+#ifndef EEGNET_RGB
+#define EEGNET_RGB 32
+#endif
+constexpr int RGB = EEGNET_RGB;   // partial rows per group reducer batch (one round trip)
+// 32-row groups, at most 16 of them (EEGNET_NGRPMAX): both levels read about the same bytes in one
+// batch each.  Against 16-row groups / 32 groups at B = 4096 the top level took 2.5-3.3 µs instead of
+// 4.2-5.2 µs per pass, the group level the same (r3 step timelines), +3 % cfg2 train trials/s.
 constexpr int FLAT_PH = 16;       // row phases per column of a one-level reduction
 constexpr long long FLAT_ELEMS = 16384;   // partial-row elements (grid x ncols) reduced in one level
 // (and grids of at most 128 rows: 512 workgroups on one ticket word serialise their atomics -- pass B
@@ -425,6 +431,15 @@ __device__ __forceinline__ void adam_slice_range(const Geo& g, int part, int npa
     i0 = min(g.nparam, lo + part * per);
     i1 = min(g.nparam, i0 + per);
 }
+// pass E's workgroup 0 computes this step's Adam scalars in its prologue and publishes them in the
+// coefficient block (CF_ADAM), so the double-precision pow()s are off the finalize's critical path
+__device__ __forceinline__ void adam_scalars_publish(const Geo& g, const FinArgs& fa) {
+    if (blockIdx.x != 0 || threadIdx.x != 0 || !adam_early(g, fa)) return;
+    float step_size, bc2s;
+    adam_scalars(fa, *fa.step + 1, step_size, bc2s);
+    pub(fa.coef + CF_ADAM * CSTR, step_size);
+    pub(fa.coef + CF_ADAM * CSTR + 1, bc2s);
+}
 __device__ void adam_slice(const Geo& g, const FinArgs& fa, int part, int nparts) {
     if (!adam_early(g, fa)) return;
     int i0, i1;
@@ -534,7 +549,12 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     TRACE_FS(g, fa.tpass, 6);
     const int s = step0 + 1;
     float step_size, bc2s;
-    adam_scalars(fa, s, step_size, bc2s);
+    if (early) {                      // adam_scalars_publish (pass E, workgroup 0): published in this launch
+        step_size = ld_pub(fa.coef + CF_ADAM * CSTR);
+        bc2s = ld_pub(fa.coef + CF_ADAM * CSTR + 1);
+    } else {
+        adam_scalars(fa, s, step_size, bc2s);
+    }
 #pragma unroll
     for (int j = 0; j < APT; ++j) {
         const int e = tid + nth * j;

@@ -643,6 +643,21 @@ int eegnet_param_count(const eegnet_dims* dims, int64_t* out) {
     return 0;
 }
 
+int eegnet_wide_spec(const eegnet_dims* dims) {
+    Geo g;
+    memset(&g, 0, sizeof(g));
+    if (int r = make_geo(dims, &g, false)) return r;
+    if (!g.wide || g.K1 != 32) return 0;
+    if (same_shape_w5(g)) return 1;
+    std::string msg = "geometry differs from EEG_SHAPE_W5:";
+    char b[96];
+#define EEG_DIFF_(f, v) if (g.f != v) { snprintf(b, sizeof(b), " %s = %d (compiled %d)", #f, (int)g.f, v); msg += b; }
+    EEG_SHAPE_W5(EEG_DIFF_)
+#undef EEG_DIFF_
+    g_err = msg;
+    return 0;
+}
+
 int eegnet_workspace_bytes(const eegnet_dims* dims, size_t* out) {
     Geo g;
     if (int r = make_geo(dims, &g)) return r;

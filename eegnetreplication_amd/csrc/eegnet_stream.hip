@@ -830,6 +830,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                          : f == 5 ? coef + CF_BO * CSTR : coef + CF_CO * CSTR;
         CT[tid] = src[o];
     }
+    adam_scalars_publish(g, fa);
     if constexpr (XDMA) barrier_vm<0>();          // first s / dp2 landed (asm DMA), pads and tables written
     else __syncthreads();
     if constexpr (!XDMA) {

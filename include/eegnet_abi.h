@@ -198,6 +198,11 @@ int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, 
 int eegnet_trace_enable(void* buf);
 size_t eegnet_trace_bytes(void);
 
+/* 1 when `dims` run the wide kernels compiled for the EEGNet-16,4 64 x 512 geometry (compile-time
+ * bounds and offsets), 0 when they run the generic wide / narrow kernels (for a wide K1 = 32 shape the
+ * differing geometry fields are then in eegnet_last_error()), < 0 on invalid dims.  No GPU needed. */
+int eegnet_wide_spec(const eegnet_dims* dims);
+
 /* sizeof(eegnet_dims) and sizeof(eegnet_fold) as this library was compiled: a binding checks its
  * struct mirrors against them at load (a stale library with another fold layout would read every
  * fold after the first from the wrong offsets). */

@@ -99,3 +99,20 @@ def test_flag_and_kernel_id_constants_match_header():
     assert flags["EEGNET_KEY_FROM_STEP"] == ops.KEY_FROM_STEP
     doc = re.search(r"i-th name eegnet_profile_collect reports:(.*?);", txt, re.S).group(1)
     assert [n.strip(" *\n") for n in doc.replace("\n", " ").split(",")] == list(_lib.KERNEL_IDS)
+
+
+def test_cfg5_runs_the_compile_time_geometry_kernels():
+    """The wide kernels compiled for EEGNet-16,4 at 64 x 512 (EEG_SHAPE_W5) are launched only when the
+    run-time geometry equals the compiled one field for field; a layout change (coefficient block,
+    workspace, LDS carve-up) that is not mirrored there would silently fall back to the generic
+    kernels (cfg5 train 1.8M -> 1.4M trials/s).  No GPU needed."""
+    import ctypes
+    from eegnetreplication_amd import _lib
+    lib = _lib.load()
+    d5 = _lib.dims(1024, 64, 512, F1=16, D=4, K1=32)
+    assert lib.eegnet_wide_spec(ctypes.byref(d5)) == 1, lib.eegnet_last_error().decode()
+    for B in (1, 7, 4096):           # the batch is a run-time field
+        d = _lib.dims(B, 64, 512, F1=16, D=4, K1=32)
+        assert lib.eegnet_wide_spec(ctypes.byref(d)) == 1
+    assert lib.eegnet_wide_spec(ctypes.byref(_lib.dims(4096, 22, 256))) == 0      # narrow
+    assert lib.eegnet_wide_spec(ctypes.byref(_lib.dims(64, 64, 256, F1=16, D=4, K1=32))) == 0
