@@ -13,7 +13,8 @@ d = json.loads(open(f"gpurun_out/ab_{os.environ['LIB']}_1.log" if False else max
 c = d.get("cfg5_train") or {}
 print(os.environ["LIB"], "cfg2 %.3fM" % (d["value"] / 1e6), "cfg5 %.4fM" % (c.get("value", 0) / 1e6),
       "folds %.3fM" % ((d.get("real_protocol_folds") or {}).get("value", 0) / 1e6),
-      {k: v["avg_us"] for k, v in (c.get("kernels") or {}).items()})
+      {k: v["avg_us"] for k, v in (c.get("kernels") or {}).items()},
+      {k: v["avg_us"] for k, v in (d.get("kernels") or {}).items()})
 PY
   done
 done

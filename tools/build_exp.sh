@@ -3,6 +3,6 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-slp-vectorize -Wno-unused-result \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared ${SLP_FLAG--fno-slp-vectorize} -Wno-unused-result \
   -Wno-unused-value ${TRACE_FLAG--DEEGNET_TRACE} "$@" -I include -o eegnetreplication_amd/libeegnet_hip_$name.so \
   eegnetreplication_amd/csrc/eegnet_kernels.hip
