@@ -493,6 +493,7 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
             const int last = ne - 1;
 #pragma unroll
             for (int j = 0; j < APT; ++j) {
+                if (nth * j >= ne) break;     // block-uniform: only the batches that hold elements
                 const int i = pidx(min(tid + nth * j, last));
                 ap[j] = fa.params[i]; am[j] = fa.adam_m[i]; av[j] = fa.adam_v[i]; ag[j] = fa.grads[i];
             }
