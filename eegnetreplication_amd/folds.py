@@ -124,10 +124,18 @@ class FoldBatch:
         dev = X0.device
         K = len(self.models)
         nsteps = (n + batch_size - 1) // batch_size
-        # any change: new tables, and the graph (which baked the old pointers in) is dropped
+        # any change: new tables, and the graph (which baked the old pointers in) is dropped.
+        # The folds' permutations and loss slots are rows of one [K, n] / [K, nsteps] buffer each:
+        # an epoch refreshes every permutation with ONE asynchronous copy from a pinned host buffer
+        # (two, alternating: the host fills the next epoch's while the device runs this one) and
+        # sums every fold's losses with one kernel.
+        perm2 = torch.zeros((K, n), dtype=torch.int64, device=dev)
+        loss2 = torch.zeros((K, nsteps), dtype=torch.float32, device=dev)
         st = {"key": key, "src": [d for d in data], "graph": None,
-              "perm": [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(K)],
-              "losses": [torch.zeros(nsteps, dtype=torch.float32, device=dev) for _ in range(K)],
+              "perm2": perm2, "perm": list(perm2.unbind(0)),
+              "loss2": loss2, "losses": list(loss2.unbind(0)),
+              "host": [torch.zeros((K, n), dtype=torch.int64).pin_memory() for _ in range(2)],
+              "copied": [None, None], "epoch": 0,
               "tables": {}, "steps": []}
         for j, i in enumerate(range(0, n, batch_size)):
             B = min(batch_size, n - i)
@@ -156,10 +164,18 @@ class FoldBatch:
     def _epoch_fused(self, data, batch_size, generators):
         n = data[0][0].shape[0]
         st = self._fused_state(data, batch_size)
+        i = st["epoch"] & 1
+        st["epoch"] += 1
+        if st["copied"][i] is not None:     # this pinned buffer's copy (two epochs ago) has run
+            st["copied"][i].synchronize()
+        host = st["host"][i]
         for k in range(len(self.models)):
             g = generators[k] if generators is not None else None
-            perm = epoch_permutation(n, g) if g is not None else torch.arange(n)
-            st["perm"][k].copy_(perm, non_blocking=True)
+            host[k].copy_(epoch_permutation(n, g) if g is not None else torch.arange(n))
+        st["perm2"].copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        st["copied"][i] = ev
         if st["graph"] is not None:
             st["graph"].replay()
         else:
@@ -172,7 +188,7 @@ class FoldBatch:
                 st["graph"] = gr
                 # the capture recorded without executing: run this epoch's work once more is NOT
                 # wanted -- the eager pass above already trained the epoch
-        return [l.sum(dtype=torch.float64) for l in st["losses"]]
+        return list(st["loss2"].sum(dim=1, dtype=torch.float64).unbind(0))
 
     def epoch(self, data: list[tuple[torch.Tensor, torch.Tensor]], batch_size: int = 64,
               generators: list[torch.Generator] | None = None) -> list[torch.Tensor]:

@@ -92,20 +92,35 @@ def _run_folds(specs, epochs, device):
     fb = FoldBatch(models, seeds, graphs=True)
     val_loss = [[] for _ in specs]
     val_acc = [[] for _ in specs]
+    # validation in groups of folds with the same validation size: one eval launch per fold, then
+    # one set of loss / accuracy reductions per group instead of per fold
+    groups = {}
+    for k, (_, yv) in enumerate(val_sets):
+        groups.setdefault(len(yv), []).append(k)
+    vgroups = []
+    for nv, ks in groups.items():
+        nb = (nv + BATCH_SIZE - 1) // BATCH_SIZE
+        seg = torch.arange(nv, device=device) // BATCH_SIZE
+        vgroups.append((ks, nb, seg, torch.bincount(seg, minlength=nb).double(),
+                        torch.stack([val_sets[k][1] for k in ks])))
     for e in range(1, epochs + 1):
         fb.epoch(train_sets, BATCH_SIZE, gens)
         with torch.no_grad():
-            for k, (m, (Xv, yv)) in enumerate(zip(models, val_sets)):
+            logits = []
+            for m, (Xv, _) in zip(models, val_sets):
                 m.eval()
-                logits = m(Xv)                      # eval BN: batch-size independent
+                logits.append(m(Xv))                # eval BN: batch-size independent
                 m.train()
-                ce = F.cross_entropy(logits, yv, reduction="none")
-                nb = (len(yv) + BATCH_SIZE - 1) // BATCH_SIZE
-                seg = torch.arange(len(yv), device=ce.device) // BATCH_SIZE
-                means = torch.zeros(nb, dtype=torch.float64, device=ce.device).index_add_(
-                    0, seg, ce.double()) / torch.bincount(seg, minlength=nb).double()
-                val_loss[k].append(means.mean())
-                val_acc[k].append((logits.argmax(1) == yv).sum())
+            for ks, nb, seg, cnt, Y in vgroups:
+                L = torch.stack([logits[k] for k in ks])                      # [G, nv, classes]
+                ce = F.cross_entropy(L.flatten(0, 1), Y.flatten(), reduction="none").view(Y.shape)
+                means = torch.zeros((len(ks), nb), dtype=torch.float64, device=ce.device).index_add_(
+                    1, seg, ce.double()) / cnt
+                vl = means.mean(1)
+                va = (L.argmax(2) == Y).sum(1)
+                for j, k in enumerate(ks):
+                    val_loss[k].append(vl[j])
+                    val_acc[k].append(va[j])
         if e == 1 or e % 50 == 0 or e == epochs:
             logger.info(f"Epoch: {e}/{epochs} ({len(specs)} folds batched)")
     out = []
