@@ -482,6 +482,7 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     auto pidx = [&](int e) { return e < na ? e : si0 + (e - na); };
     float ap[APT], am[APT], av[APT], ag[APT];
     int step0;
+    float es0 = 0.f, es1 = 0.f;
     {
         Stage<3, double> s0;
         Stage<1, float> s1;
@@ -499,6 +500,10 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
             }
         }
         step0 = adam ? *fa.step : 0;
+        if (early) {                  // adam_scalars_publish (pass E, workgroup 0), in this batch
+            es0 = ld_pub(fa.coef + CF_ADAM * CSTR);
+            es1 = ld_pub(fa.coef + CF_ADAM * CSTR + 1);
+        }
         s0.store(Gm, K1 * K1 + K1);
         s1.store(wd, F1 * K1);
         s2.store(cf, CF_COUNT * CSTR);
@@ -551,8 +556,8 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     const int s = step0 + 1;
     float step_size, bc2s;
     if (early) {                      // adam_scalars_publish (pass E, workgroup 0): published in this launch
-        step_size = ld_pub(fa.coef + CF_ADAM * CSTR);
-        bc2s = ld_pub(fa.coef + CF_ADAM * CSTR + 1);
+        step_size = es0;
+        bc2s = es1;
     } else {
         adam_scalars(fa, s, step_size, bc2s);
     }

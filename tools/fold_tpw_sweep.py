@@ -33,4 +33,5 @@ def run(n_folds, n_train=1440, epochs=2, dev="cuda:0"):
 if __name__ == "__main__":
     tpw = os.environ.get("EEGNET_FOLD_TPW", "default")
     for nf in [int(a) for a in sys.argv[1:]] or [90, 12]:
-        print(f"tpw {tpw} folds {nf}: {run(nf) / 1e6:.3f} M trials/s", flush=True)
+        print(f"tpw {tpw} folds {nf}: {run(nf, epochs=int(os.environ.get('EPOCHS', 2))) / 1e6:.3f} M trials/s",
+              flush=True)
