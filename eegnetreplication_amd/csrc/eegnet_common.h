@@ -488,6 +488,19 @@ __device__ __forceinline__ void wave_reduce(float (&v)[N]) {
     for (int j = 0; j < N / 4; ++j) v[j] = row_sum16(v[j]);
 }
 
+// column c of a workgroup's per-wave partial rows red[w][stride], w < nw <= NWMAX, summed in wave
+// order: every row's LDS read issues before the first add (one LDS round trip, not nw)
+template <int NWMAX>
+__device__ __forceinline__ float wave_rows_sum(const float* red, int nw, int stride, int c) {
+    float v[NWMAX];
+#pragma unroll
+    for (int w = 0; w < NWMAX; ++w) v[w] = red[min(w, nw - 1) * stride + c];
+    float a = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWMAX; ++w) a += w < nw ? v[w] : 0.f;
+    return a;
+}
+
 // order this wave's LDS writes before its later LDS reads (rows a wave owns need no block barrier)
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

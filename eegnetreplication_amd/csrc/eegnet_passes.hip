@@ -333,11 +333,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     }
     __syncthreads();
     float* row = part + (size_t)blockIdx.x * g.nC;
-    for (int c = tid; c < g.nC; c += blockDim.x) {
-        float a = 0.f;
-        for (int w = 0; w < nw; ++w) a += red[w * g.nC + c];
-        pub(row + c, a);
-    }
+    for (int c = tid; c < g.nC; c += blockDim.x) pub(row + c, wave_rows_sum<NTH / 64>(red, nw, g.nC, c));
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
 }
@@ -595,11 +591,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
     }
     __syncthreads();
     float* row = part + (size_t)blockIdx.x * g.nD;
-    for (int c = tid; c < g.nD; c += blockDim.x) {
-        float a = 0.f;
-        for (int w = 0; w < nw; ++w) a += red[w * g.nD + c];
-        pub(row + c, a);
-    }
+    for (int c = tid; c < g.nD; c += blockDim.x) pub(row + c, wave_rows_sum<NTHS / 64>(red, nw, g.nD, c));
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
 }
