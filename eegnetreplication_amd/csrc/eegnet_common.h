@@ -290,6 +290,9 @@ __device__ __forceinline__ FinArgs fold_fin(const FoldCall& fc, const eegnet_fol
 // padded-row strides, shared by host (make_geo) and the compile-time-shape kernels
 __host__ __device__ constexpr int rup4(int a) { return (a + 3) & ~3; }
 __host__ __device__ constexpr int imax(int a, int b) { return a > b ? a : b; }
+// row pitch of the s plane [B][F2][s_pitch(T)] (floats): T rounded up to 4, so rows are 16-byte units
+__host__ __device__ constexpr int s_pitch(int T) { return (T + 3) & ~3; }
+
 __host__ __device__ constexpr int row_stride(int K1, int T) {
     // rows of x / s / dy / e: [LP zeros | T samples | >= R zeros]; long enough for the last 4-output
     // FIR window, the last 16-column MFMA tile and the last lag-correlation B tile of pass E; RS/4 odd so that column reads of 16 rows (MFMA

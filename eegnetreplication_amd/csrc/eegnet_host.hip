@@ -244,7 +244,7 @@ static WsLayout make_layout(const Geo& g) {
     L.d2 = take(per); L.E1 = take(per); L.E2 = take(per); L.dp2 = take(per);
     L.dl = take((size_t)g.B * NCLS * 4);
     // pass A's s [B][F2][T] and v [B][F2][8 ceil(T/8)] planes, read back by passes B and E
-    L.s = take((size_t)g.B * g.F2 * g.T * 4);
+    L.s = take((size_t)g.B * g.F2 * s_pitch(g.T) * 4);
     L.v = take((size_t)g.B * g.F2 * ((g.T + 7) / 8 * 8) * 4);
     // F2 <= 16: pass B's block-2 depthwise output q and pointwise output r [B][F2][T/4], read by passes
     // C (r) and D (q, r) instead of recomputing them from d2

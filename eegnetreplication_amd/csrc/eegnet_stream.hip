@@ -142,21 +142,26 @@ __device__ __forceinline__ void barrier_vm() {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(N) : "memory");
 }
 
-// one trial's s rows (LDS, [LP | T samples] per row) -> a contiguous [F2][T] block in global memory
+// one trial's s rows (LDS, [LP | T samples] per row) -> a contiguous [F2][s_pitch(T)] block in global
+// memory.  The s plane's rows are padded to s_pitch(T) floats (eegnet_common.h), zeros after T (the LDS rows'
+// right pads), so every shape stores and DMAs them in 16-byte units (22 x 257: 65 float4 per row
+// instead of 257 dwords).
 template <int NT>
 __device__ __forceinline__ void s_rows_store(const float* Ss, float* __restrict__ sb, int F2, int T, int RS, int LP,
                                              int tid) {
-    if ((T & 3) == 0) {
-        const int TQ4 = T >> 2;
-        for (int i = tid; i < F2 * TQ4; i += NT) {
-            const int o = i / TQ4, q = i - o * TQ4;
-            __builtin_nontemporal_store(lds_ld4(Ss + o * RS + LP + 4 * q), reinterpret_cast<floatx4*>(sb + 4 * i));
-        }
-    } else {
-        for (int i = tid; i < F2 * T; i += NT) {
-            const int o = i / T, t = i - o * T;
-            sb[i] = Ss[o * RS + LP + t];
-        }
+    const int TQ4 = s_pitch(T) >> 2;
+    for (int i = tid; i < F2 * TQ4; i += NT) {
+        const int o = i / TQ4, q = i - o * TQ4;
+        __builtin_nontemporal_store(lds_ld4(Ss + o * RS + LP + 4 * q), reinterpret_cast<floatx4*>(sb + 4 * i));
+    }
+}
+// rows [0, rows) of one trial's s plane into LDS rows (stride RS, left pad LP), 16-byte LDS-DMA units
+__device__ __forceinline__ void s_dma_asm(const float* __restrict__ sb, int rows, int T, int RS, int LP, float* Ss,
+                                          int wave, int lane) {
+    const int TS = s_pitch(T), np = (TS + 255) >> 8;
+    for (int i = wave; i < rows * np; i += NWB) {
+        const int c = i / np, p = i - c * np;
+        if (4 * lane < TS - 256 * p) dma16(sb + (size_t)c * TS + 256 * p + 4 * lane, Ss + c * RS + LP + 256 * p);
     }
 }
 
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         }
         TRACE_PH(g, 0, 1, tph_);
         // s rows -> the s plane [B][F2][T] (pass E's lag-correlation operand)
-        s_rows_store<NTB>(Ss, sg + (size_t)b * F2 * T, F2, T, RS, LP, tid);
+        s_rows_store<NTB>(Ss, sg + (size_t)b * F2 * s_pitch(T), F2, T, RS, LP, tid);
         // v = 32-tap FIR of this wave's s rows; BN2 sums of v; v -> the v plane [B][F2][8 NO] (passes
         // B and E read it back instead of recomputing the spatial GEMM and the FIR).  Compile-time
         // shapes hold v in registers across the trial's closing barrier and store it after, so the
@@ -772,7 +777,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         if constexpr (!XDMA) {
 #pragma unroll
             for (int r = 0; r < RPW; ++r) {
-                const float* src = sg + ((size_t)bb * F2 + min(RPW * wave + r, F2 - 1)) * T;
+                const float* src = sg + ((size_t)bb * F2 + min(RPW * wave + r, F2 - 1)) * s_pitch(T);
 #pragma unroll
                 for (int k = 0; k < MS; ++k) pws[r][k] = src[min(lane + 64 * k, T - 1)];
             }
@@ -805,7 +810,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     // before anything else; the pad fill, the tap / coefficient loads overlap them and one barrier
     // waits for all of it (in sequence these were four dependent round trips, ~6 us of prologue)
     if (b0 < b1) {
-        if constexpr (XDMA) x_dma_asm(sg + (size_t)b0 * F2 * T, F2, T, RS, LP, Ss, wave, lane);
+        if constexpr (XDMA) s_dma_asm(sg + (size_t)b0 * F2 * s_pitch(T), F2, T, RS, LP, Ss, wave, lane);
         else s_rows_load(b0);
         TRACE_PS(g, 3);
         if constexpr (DPDMA) flat_dma_asm(dp2g + (size_t)b0 * ndp, ndp, DP, wave, lane);
@@ -950,7 +955,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
 #pragma unroll
                         for (int r = 0; r < RPW; ++r) {
                             const int o = RPW * wave + r;
-                            dma16(sg + ((size_t)bn * F2 + o) * T + 4 * lane, Ss + o * RS + LP);
+                            dma16(sg + ((size_t)bn * F2 + o) * s_pitch(T) + 4 * lane, Ss + o * RS + LP);
                         }
                     }
                 }
@@ -1053,7 +1058,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         else __syncthreads();
         TRACE_PH(g, 4, 4, tph_);
         if (!PIPEE && bn < b1) {
-            if constexpr (XDMA) x_dma_asm(sg + (size_t)bn * F2 * T, F2, T, RS, LP, Ss, wave, lane);
+            if constexpr (XDMA) s_dma_asm(sg + (size_t)bn * F2 * s_pitch(T), F2, T, RS, LP, Ss, wave, lane);
             else {                                         // registers over the dws GEMM only
                 s_rows_load(bn);
                 x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * T), C, T, pfx, tid);

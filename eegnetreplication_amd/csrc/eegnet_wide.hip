@@ -251,7 +251,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 __builtin_nontemporal_store((floatx4){v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
                 __builtin_nontemporal_store((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
             }
-            float* srow = sg + ((size_t)b * F2 + o) * T;
+            float* srow = sg + ((size_t)b * F2 + o) * s_pitch(T);
             if ((T & 3) == 0) {
                 for (int t = 4 * lane; t < T; t += 256)
                     __builtin_nontemporal_store(lds_ld4(row + LP + t), reinterpret_cast<floatx4*>(srow + t));
@@ -1103,7 +1103,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
     const bool rdma = (T & 255) == 0;
     auto stage_rows = [&](int bb) {
         if (!row_on) return;
-        const float* srow = sg + ((size_t)bb * F2 + o) * T;
+        const float* srow = sg + ((size_t)bb * F2 + o) * s_pitch(T);
         const float* drow = dp2g + ((size_t)bb * F2 + o) * T1;
         if (rdma) {
             for (int p = 0; p < (T >> 8); ++p) dma16(srow + 256 * p + 4 * lane, Ss + wave * RS + LP + 256 * p);
