@@ -31,6 +31,7 @@ class Dims(ctypes.Structure):
         ("B", ctypes.c_int), ("C", ctypes.c_int), ("T", ctypes.c_int),
         ("F1", ctypes.c_int), ("D", ctypes.c_int), ("K1", ctypes.c_int),
         ("p_drop", ctypes.c_float), ("bn_eps", ctypes.c_float), ("bn_momentum", ctypes.c_float),
+        ("x_pitch", ctypes.c_int),
     ]
 
 
@@ -67,6 +68,7 @@ _SIGS = {
     "eegnet_trace_bytes": (ctypes.c_size_t, []),
     "eegnet_dims_bytes": (ctypes.c_size_t, []),
     "eegnet_wide_spec": (ctypes.c_int, [ctypes.POINTER(Dims)]),
+    "eegnet_x_pitch": (ctypes.c_int, [ctypes.POINTER(Dims)]),
     "eegnet_fold_bytes": (ctypes.c_size_t, []),
     "eegnet_last_error": (ctypes.c_char_p, []),
     "eegnet_build_info": (ctypes.c_char_p, []),
@@ -106,9 +108,9 @@ def check(rc: int, what: str):
         raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
 
 
-def dims(B, C, T, F1=8, D=2, K1=32, p=0.5, eps=1e-5, momentum=0.1) -> Dims:
+def dims(B, C, T, F1=8, D=2, K1=32, p=0.5, eps=1e-5, momentum=0.1, x_pitch=0) -> Dims:
     return Dims(int(B), int(C), int(T), int(F1), int(D), int(K1), float(p), float(eps),
-                float(momentum))
+                float(momentum), int(x_pitch))
 
 
 def param_count(d: Dims) -> int:

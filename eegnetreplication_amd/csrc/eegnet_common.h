@@ -74,6 +74,7 @@ struct Geo {
     // step with synchronised BatchNorm (eegnet_train_stage), whose per-pass sums are all-reduced
     int Bn;
     int defer;           // the reduction's winner leaves the pass's sums in part2 row 0; no finalize
+    int XP;              // x row pitch (floats between channel rows; T unless eegnet_dims.x_pitch)
 };
 
 // Compile-time cfg5 geometry (EEGNet-16,4 at 64ch x 512, K1 = 32): the shape fields make_geo computes

@@ -87,6 +87,11 @@ static int grid_mult_cd() {
     return m;
 }
 
+// the compile-time shapes of the narrow passes (EEG_DISPATCH), whose x loads honour a row pitch
+static bool x_pitch_shape(const eegnet_dims& d) {
+    return d.K1 == 32 && d.C == 22 && (d.T == 256 || d.T == 257) && d.F1 == 8 && d.D == 2;
+}
+
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     if (!d) return fail(EEGNET_EINVAL, "dims is NULL");
     memset(g, 0, sizeof(*g));
@@ -101,6 +106,10 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
         return fail(EEGNET_EINVAL, "F1*D must be a multiple of 4 in [4,64] (got F1=%d D=%d)", g->F1, g->D);
     if (g->T < 32 || g->T < g->K1 || g->T > 1024)
         return fail(EEGNET_EINVAL, "T must be in [max(32,K1), 1024] (got %d)", g->T);
+    g->XP = d->x_pitch ? d->x_pitch : g->T;
+    if (g->XP != g->T && !(x_pitch_shape(*d) && (g->XP & 3) == 0 && g->XP > g->T))
+        return fail(EEGNET_EINVAL, "x_pitch %d: only the 22 x 256 / 257 EEGNet-8,2 (K1 = 32) training kernels take "
+                    "a row pitch, a multiple of 4 above T (eegnet_x_pitch)", g->XP);
     g->P = (g->K1 - 1) / 2; g->R = g->K1 - 1 - g->P;
     g->T1 = g->T / 4; g->T2 = g->T1 / 8; g->NF = g->F2 * g->T2;
     g->LP = (g->R + 3) & ~3;
@@ -643,6 +652,11 @@ int eegnet_param_count(const eegnet_dims* dims, int64_t* out) {
     return 0;
 }
 
+int eegnet_x_pitch(const eegnet_dims* dims) {
+    if (!dims) return fail(EEGNET_EINVAL, "dims is NULL");
+    return x_pitch_shape(*dims) && (dims->T & 3) ? (dims->T + 3) & ~3 : dims->T;
+}
+
 int eegnet_wide_spec(const eegnet_dims* dims) {
     Geo g;
     memset(&g, 0, sizeof(g));
@@ -731,6 +745,7 @@ int eegnet_forward_eval(const eegnet_dims* dims, const float* params, const floa
                         const float* x, float* logits, void* stream) {
     Geo g;
     if (int r = make_geo(dims, &g)) return r;
+    if (g.XP != g.T) return fail(EEGNET_EINVAL, "the eval forward takes x as [B][C][T] (x_pitch 0 or T)");
     if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
     if (int r = check_ptrs(x, "x", logits, "logits")) return r;
     ensure_attrs();
@@ -755,6 +770,8 @@ int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const
                              const uint16_t* x, float* logits, void* stream) {
     GeoI g;
     if (int r = make_geo_bf16(dims, &g)) return r;
+    if (dims->x_pitch && dims->x_pitch != dims->T)
+        return fail(EEGNET_EINVAL, "the eval forward takes x as [B][C][T] (x_pitch 0 or T)");
     if (int r = check_ptrs(params, "params", bn_buffers, "bn_buffers")) return r;
     if (int r = check_ptrs(x, "x", logits, "logits")) return r;
     if (g.PFU > 0 && ((uintptr_t)x & 15))

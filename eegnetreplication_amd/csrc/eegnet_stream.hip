@@ -74,19 +74,32 @@ __device__ __forceinline__ void dma4(const float* gsrc, const float* ldst) {    
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
                  :: "v"(gsrc), "s"(la) : "memory", "m0");
 }
-__device__ __forceinline__ void x_dma_asm(const float* __restrict__ xb, int C, int T, int RS, int LP, float* Xs,
-                                          int wave, int lane) {
-    if ((T & 255) == 0) {
+// C rows of T samples at row pitch XP (floats) into LDS rows (stride RS, left pad LP).  Rows at a pitch
+// that is a multiple of 4 go in 16-byte units -- 4 [T/4] of them, then T mod 4 dwords -- else in dwords
+// (a 257-sample row at pitch 257 is not 16-byte aligned: five dword DMAs per row instead of two).
+__device__ __forceinline__ void x_dma_asm(const float* __restrict__ xb, int C, int T, int XP, int RS, int LP,
+                                          float* Xs, int wave, int lane) {
+    if ((T & 255) == 0 && (XP & 3) == 0) {
         const int np = T >> 8;
         for (int i = wave; i < C * np; i += NWB) {
             const int c = i / np, p = i - c * np;
-            dma16(xb + (size_t)c * T + 256 * p + 4 * lane, Xs + c * RS + LP + 256 * p);
+            dma16(xb + (size_t)c * XP + 256 * p + 4 * lane, Xs + c * RS + LP + 256 * p);
+        }
+    } else if ((XP & 3) == 0) {
+        const int nu = T >> 2, np = (nu + 63) >> 6, nt = T & 3, per = np + (nt ? 1 : 0);
+        for (int i = wave; i < C * per; i += NWB) {
+            const int c = i / per, p = i - c * per;
+            if (p < np) {
+                if (lane < nu - 64 * p) dma16(xb + (size_t)c * XP + 256 * p + 4 * lane, Xs + c * RS + LP + 256 * p);
+            } else if (lane < nt) {
+                dma4(xb + (size_t)c * XP + 4 * nu + lane, Xs + c * RS + LP + 4 * nu);
+            }
         }
     } else {
         const int np = (T + 63) >> 6;
         for (int i = wave; i < C * np; i += NWB) {
             const int c = i / np, p = i - c * np;
-            if (lane < T - 64 * p) dma4(xb + (size_t)c * T + 64 * p + lane, Xs + c * RS + LP + 64 * p);
+            if (lane < T - 64 * p) dma4(xb + (size_t)c * XP + 64 * p + lane, Xs + c * RS + LP + 64 * p);
         }
     }
 }
@@ -255,7 +268,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     // compile-time shapes: the first trial's x goes out by LDS-DMA before anything else; the pad fill,
     // the weight loads and the edge decode below overlap it, and one barrier waits for all of it
     if constexpr (XDMA) {
-        if (b0 < b1) x_dma_asm(x + fold_row(perm, row0, b0) * (C * T), C, T, RS, LP, Xb, wave, lane);
+        if (b0 < b1) x_dma_asm(x + fold_row(perm, row0, b0) * (C * g.XP), C, T, g.XP, RS, LP, Xb, wave, lane);
         zero_pads(sm, C + F2, RS, LP, T, tid);
     } else {
         zero_fill<false>(sm, (C + F2) * RS, C, RS, LP, T, tid);
@@ -298,7 +311,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     if constexpr (XDMA) {
         barrier_vm<0>();                              // the first x landed, pads and tables written
     } else {
-        if (b0 < b1) x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * T), C, T, pf, tid);
+        if (b0 < b1) x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * g.XP), C, T, pf, tid);
         __syncthreads();
         x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         __syncthreads();
@@ -354,8 +367,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         barrier_lds();                                     // Ss complete, x read for good (LDS only:
                                                            // the previous trial's v stores stay in flight)
         if (bn < b1) {                                     // next x: lands by the closing barrier
-            if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, bn) * (C * T), C, T, RS, LP, Xb, wave, lane);
-            else x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * T), C, T, pf, tid);   // live over the FIR only
+            if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, bn) * (C * g.XP), C, T, g.XP, RS, LP, Xb, wave, lane);
+            else x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * g.XP), C, T, pf, tid);   // live over the FIR only
         }
         TRACE_PH(g, 0, 1, tph_);
         // s rows -> the s plane [B][F2][T] (pass E's lag-correlation operand)
@@ -841,7 +854,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     if constexpr (!XDMA) {
         if (b0 < b1) {
             s_rows_put();
-            x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * T), C, T, pfx, tid);
+            x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * g.XP), C, T, pfx, tid);
             x_store<PF, NTB>(pfx, C, T, RS, LP, Xb, tid);
         }
         __syncthreads();
@@ -909,7 +922,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         }
         // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
         // GEMM); they land during the lag correlation / FIR^T, by the next barrier
-        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * T), C, T, RS, LP, Xb, wave, lane);
+        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * g.XP), C, T, g.XP, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 2, tph_);
         {
             float tl[K1];
@@ -1061,7 +1074,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             if constexpr (XDMA) s_dma_asm(sg + (size_t)bn * F2 * s_pitch(T), F2, T, RS, LP, Ss, wave, lane);
             else {                                         // registers over the dws GEMM only
                 s_rows_load(bn);
-                x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * T), C, T, pfx, tid);
+                x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * g.XP), C, T, pfx, tid);
             }
             if constexpr (DPDMA) flat_dma_asm(dp2g + (size_t)bn * ndp, ndp, DP, wave, lane);
             asm volatile("" ::: "memory");                 // the v loads issue after the DMA (barrier_vm)

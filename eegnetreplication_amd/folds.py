@@ -137,6 +137,19 @@ class FoldBatch:
               "host": [torch.zeros((K, n), dtype=torch.int64).pin_memory() for _ in range(2)],
               "copied": [None, None], "epoch": 0,
               "tables": {}, "steps": []}
+        # x rows at the pitch the kernels load fastest (22 x 257: 260 floats, 16-byte DMA units):
+        # one padded copy per distinct X, kept for the life of this state
+        shape = self.models[0].shape
+        xp = shape.x_pitch()
+        st["x_pitch"] = 0 if xp == shape.T else xp
+        st["xpad"] = {}
+
+        def xrows(X):
+            if ops.x_pitch_of(X) == st["x_pitch"]:
+                return X
+            if id(X) not in st["xpad"]:
+                st["xpad"][id(X)] = ops.pad_x_rows(X, xp)
+            return st["xpad"][id(X)]
         for j, i in enumerate(range(0, n, batch_size)):
             B = min(batch_size, n - i)
             st["steps"].append((i, j, B))
@@ -147,7 +160,7 @@ class FoldBatch:
                     # x / labels stay unshuffled: the kernels read batch row r as row perm[r]
                     X, y = data[k]
                     ents.append(dict(params=m.flat_parameters(), bn_buffers=m.flat_bn_buffers(),
-                                     num_batches_tracked=m.flat_num_batches_tracked(), x=X, labels=y,
+                                     num_batches_tracked=m.flat_num_batches_tracked(), x=xrows(X), labels=y,
                                      perm=st["perm"][k], grads=a.grads, adam_state=a.state, step=a.step,
                                      losses=st["losses"][k], ws=self._workspace(k, B), seed=self.seeds[k]))
                 st["tables"][B] = ops.fold_table(ents, dev)
@@ -159,7 +172,7 @@ class FoldBatch:
         K = len(self.models)
         for i, j, B in st["steps"]:
             ops.train_step_folds(shape, B, st["tables"][B], K, row0=i, slot=j, offset=0, lr=self.lr,
-                                 betas=self.betas, eps=self.eps)
+                                 betas=self.betas, eps=self.eps, x_pitch=st["x_pitch"])
 
     def _epoch_fused(self, data, batch_size, generators):
         n = data[0][0].shape[0]

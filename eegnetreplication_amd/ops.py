@@ -55,15 +55,20 @@ class Shape:
     def T2(self):
         return self.T1 // 8
 
-    def dims(self, B: int, p: float | None = None) -> _lib.Dims:
-        if p is None:                 # per-B cache (the struct is only read by the library)
+    def dims(self, B: int, p: float | None = None, x_pitch: int = 0) -> _lib.Dims:
+        if p is None:                 # per-(B, pitch) cache (the struct is only read by the library)
             cache = self.__dict__.setdefault("_dims_cache", {})
-            d = cache.get(B)
+            d = cache.get((B, x_pitch))
             if d is None:
-                d = cache[B] = _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1, self.p, self.eps,
-                                         self.momentum)
+                d = cache[(B, x_pitch)] = _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1, self.p,
+                                                    self.eps, self.momentum, x_pitch)
             return d
-        return _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1, p, self.eps, self.momentum)
+        return _lib.dims(B, self.C, self.T, self.F1, self.D, self.K1, p, self.eps, self.momentum, x_pitch)
+
+    def x_pitch(self) -> int:
+        """The x row pitch the training kernels load fastest (eegnet_x_pitch): T rounded up to 4
+        floats for 22 x 257, else T."""
+        return int(_lib.load().eegnet_x_pitch(ctypes.byref(self.dims(1))))
 
     def param_shapes(self):
         """(name, shape) in nn.Module.named_parameters() order (model.py:22-84)."""
@@ -169,12 +174,35 @@ def adam_step(params, grads, exp_avg, exp_avg_sq, step_i32, lr=1e-3, betas=(0.9,
         ctypes.c_float(eps), _stream()), "eegnet_adam_step")
 
 
+def x_pitch_of(x: torch.Tensor) -> int:
+    """eegnet_dims.x_pitch for x: 0 for a contiguous [B, C, T] tensor, the channel-row pitch for a
+    [B, C, T] view of [B, C, pitch] rows (``pad_x_rows``)."""
+    if x.is_contiguous():
+        return 0
+    B, C, T = x.shape
+    if x.stride(2) != 1 or x.stride(0) != C * x.stride(1) or x.stride(1) < T:
+        raise ValueError("x must be a contiguous [B, C, T] tensor or a [B, C, T] view of [B, C, pitch] rows")
+    return int(x.stride(1))
+
+
+def pad_x_rows(x: torch.Tensor, pitch: int) -> torch.Tensor:
+    """A copy of x [N, C, T] with its rows at ``pitch`` floats (zeros after T), returned as the
+    [N, C, T] view the training entry points take (x_pitch_of): 22 x 257 trials then load in 16-byte
+    units."""
+    N, C, T = x.shape
+    if pitch == T:
+        return x.contiguous()
+    xp = torch.zeros((N, C, pitch), dtype=x.dtype, device=x.device)
+    xp[:, :, :T] = x
+    return xp[:, :, :T]
+
+
 def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset: int, grads,
                adam_state, step_i32, ws, loss, logits=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-7,
                p: float | None = None, clamp=True, nbt=None, key_from_step=False):
     """One fused hot-loop iteration (model.py:141-148) on the device, no host sync.
     ``adam_state=None`` stops after the gradients (data-parallel)."""
-    d = shape.dims(x.shape[0], p)
+    d = shape.dims(x.shape[0], p, x_pitch_of(x))
     _lib.check(_lib.load().eegnet_train_step(
         ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(labels),
         ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),
@@ -227,11 +255,13 @@ def fold_table(entries, device) -> torch.Tensor:
 
 
 def train_step_folds(shape: Shape, B: int, table: torch.Tensor, nfolds: int, row0: int, slot: int,
-                     offset: int = 0, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, p: float | None = None):
+                     offset: int = 0, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, p: float | None = None,
+                     x_pitch: int = 0):
     """eegnet_train_step_folds: one fused step of ``nfolds`` independent models in one launch per
     pass (fold index = grid y).  ``table`` from fold_table(); every fold trains on rows
-    [row0, row0 + B) of its own x / labels and writes its loss to losses[slot]."""
-    d = shape.dims(B, p)
+    [row0, row0 + B) of its own x / labels and writes its loss to losses[slot].  ``x_pitch``: the
+    row pitch of every fold's x (0: contiguous [N, C, T]; pad_x_rows)."""
+    d = shape.dims(B, p, x_pitch)
     _lib.check(_lib.load().eegnet_train_step_folds(
         ctypes.byref(d), ctypes.c_int(nfolds), _ptr(table), ctypes.c_int64(row0), ctypes.c_int64(slot),
         ctypes.c_uint64(offset), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),

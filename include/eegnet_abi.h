@@ -50,6 +50,9 @@ typedef struct eegnet_dims {
     float p_drop;   /* dropout p             (model.py:13, 50, 74)          */
     float bn_eps;   /* BatchNorm2d eps (1e-5)                               */
     float bn_momentum; /* BatchNorm2d momentum (0.1)                        */
+    int x_pitch;    /* floats between consecutive channel rows of x (0: T, x is [B][C][T]); a
+                       larger pitch (eegnet_x_pitch) lets the training kernels load the rows of
+                       x in 16-byte units; samples [T, x_pitch) of a row are never read     */
 } eegnet_dims;
 
 enum {
@@ -197,6 +200,12 @@ int eegnet_profile_collect(char* names, int* counts, double* total_ms, int cap, 
  * finalize, shader-clock sums of in-loop phases).  NULL turns it off. */
 int eegnet_trace_enable(void* buf);
 size_t eegnet_trace_bytes(void);
+
+/* The x row pitch the training entry points (eegnet_train_step, _folds, _forward_train, _backward,
+ * _train_stage) load fastest for `dims`: T rounded up to 4 floats when the kernels for these dims take
+ * x rows in 16-byte units at such a pitch (22 x 257, the recordings' shape: a 257-float row is not
+ * 16-byte aligned), else T.  Every other entry point needs x_pitch = 0 or T.  No GPU needed. */
+int eegnet_x_pitch(const eegnet_dims* dims);
 
 /* 1 when `dims` run the wide kernels compiled for the EEGNet-16,4 64 x 512 geometry (compile-time
  * bounds and offsets), 0 when they run the generic wide / narrow kernels (for a wide K1 = 32 shape the

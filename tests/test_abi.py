@@ -116,3 +116,24 @@ def test_cfg5_runs_the_compile_time_geometry_kernels():
         assert lib.eegnet_wide_spec(ctypes.byref(d)) == 1
     assert lib.eegnet_wide_spec(ctypes.byref(_lib.dims(4096, 22, 256))) == 0      # narrow
     assert lib.eegnet_wide_spec(ctypes.byref(_lib.dims(64, 64, 256, F1=16, D=4, K1=32))) == 0
+
+
+def test_x_pitch_entry_point_and_validation():
+    """eegnet_x_pitch: 260 for the recordings' 22 x 257 EEGNet-8,2 (16-byte rows), T elsewhere; a
+    pitch is accepted only where the kernels honour it (checked by the geometry, no GPU needed)."""
+    import ctypes
+    from eegnetreplication_amd import _lib
+    lib = _lib.load()
+    xp = lambda *a, **k: lib.eegnet_x_pitch(ctypes.byref(_lib.dims(*a, **k)))
+    assert xp(64, 22, 257) == 260
+    assert xp(64, 22, 256) == 256
+    assert xp(64, 22, 257, K1=64) == 257
+    assert xp(64, 32, 257) == 257
+    assert xp(64, 64, 512, F1=16, D=4) == 512
+    nb = ctypes.c_size_t()
+    ok = lambda d: lib.eegnet_workspace_bytes(ctypes.byref(d), ctypes.byref(nb))
+    assert ok(_lib.dims(64, 22, 257, x_pitch=260)) == 0
+    assert ok(_lib.dims(64, 22, 257, x_pitch=257)) == 0
+    assert ok(_lib.dims(64, 22, 257, x_pitch=258)) != 0          # not a multiple of 4
+    assert ok(_lib.dims(64, 22, 257, x_pitch=256)) != 0          # below T
+    assert ok(_lib.dims(64, 32, 257, x_pitch=260)) != 0          # a runtime-shape kernel

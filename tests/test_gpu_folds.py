@@ -246,3 +246,26 @@ def test_fused_fold_launch_equals_per_fold_streams(graphs):
                 assert torch.equal(a, b), f"epoch {e} fold {k}: 5-fold launch differs from the fold alone"
     assert fused._fz is not None and (fused._fz["graph"] is not None) == graphs
     assert int(fused.adam[0].step.item()) == 3 * 3
+
+
+@pytest.mark.parametrize("B", [64, 1440])
+def test_padded_x_rows_bit_identical(B):
+    """x rows at pitch 260 (ops.pad_x_rows; the 22 x 257 kernels then DMA them in 16-byte units plus
+    one trailing dword instead of five dword pieces) train bit-identically to contiguous x: same
+    parameters, BN buffers, Adam state and losses over three fused steps."""
+    from eegnetreplication_amd import FusedTrainer, ops
+    dev = _dev()
+    X, y = _data(B, 11, dev)
+    assert _models(1, 0.5, dev)[0].shape.x_pitch() == 260
+    Xp = ops.pad_x_rows(X, 260)
+    assert ops.x_pitch_of(Xp) == 260 and torch.equal(Xp, X)
+    outs = []
+    for xin in (X, Xp):
+        m = _models(1, 0.5, dev)[0]
+        tr = FusedTrainer(m)
+        losses = [tr.step(xin, y).clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        outs.append((m.flat_parameters().clone(), m.flat_bn_buffers().clone(), tr.adam.state.clone(),
+                     torch.cat(losses)))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
