@@ -79,6 +79,9 @@ def test_integration_ctypes_example_matches_binding():
     m = re.search(r"lib\.eegnet_train_step\.argtypes = \[(.*?)\]\n", txt, re.S)
     n_decl = m.group(1).count(",") + 1
     assert n_decl == len(_lib._SIGS["eegnet_train_step"][1]) == _header_param_count("eegnet_train_step")
+    fields = re.findall(r'\("(\w+)", ctypes\.c_(?:int|float)\)', re.search(r"class Dims\(ctypes\.Structure\):(.*?)\]\n",
+                                                                    txt, re.S).group(1))
+    assert fields == [n for n, _ in _lib.Dims._fields_]          # the struct mirror, field for field
     call = re.search(r"rc = lib\.eegnet_train_step\((.*?)\)\s*(?:#.*)?\n(?=if rc)", txt, re.S).group(1)
     call = re.sub(r"#[^\n]*", "", call)
     depth, n_args = 0, 1
