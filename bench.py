@@ -267,10 +267,11 @@ def cpu_model_name():
 
 
 def cpu_baseline(B, C, T, steps, threads, real_loop=False):
-    """Reference CPU path (stock ATen via oracle/torch_ref.py) on this host; trials/s.
-    ``real_loop``: the reference's own loop body (model.py:136-148) -- float64 batch from the
-    loader, ``signals.float()``, forward, CE, ``loss.item()`` (a sync per step), zero_grad,
-    backward, Adam step."""
+    """Reference CPU path (stock ATen via oracle/torch_ref.py) on this host; trials/s over the median
+    of ``steps`` individually timed steps after one warm-up.  ``real_loop``: the reference's own loop
+    body (model.py:136-148) -- float64 batch from the loader, ``signals.float()``, forward, CE,
+    ``loss.item()`` (a sync per step), zero_grad, backward, Adam step.  Returns (trials/s at the
+    median step, total timed seconds, per-step seconds)."""
     from oracle import torch_ref as tr
     from eegnetreplication_amd import EEGNet
     prev = torch.get_num_threads()
@@ -291,43 +292,66 @@ def cpu_baseline(B, C, T, steps, threads, real_loop=False):
                 loss.item()
 
         one()                                    # warm-up
-        t0 = time.perf_counter()
+        times = []
         for _ in range(steps):
+            t0 = time.perf_counter()
             one()
-        dt = time.perf_counter() - t0
+            times.append(time.perf_counter() - t0)
     finally:
         torch.set_num_threads(prev)
-    return B * steps / dt, dt
+    return B / float(np.median(times)), float(sum(times)), times
+
+
+def host_cpu_info():
+    """lscpu's model / topology lines (record the host's CPU), or /proc/cpuinfo's
+    model name when lscpu is missing."""
+    import subprocess
+    keep = ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)", "NUMA node(s)")
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        info = {}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in keep:
+                info[k.strip()] = v.strip()
+        if info:
+            return info
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return {"Model name": cpu_model_name()}
 
 
 def cpu_baselines(C, T, B, steps):
-    """The cfg2 step at B (best of 1 and 16 threads: the box's CPU share for one GPU is 16; the
-    B = 4096 step's 738 MB intermediates make it memory-bound, so threads help little) and the
-    reference's real loop at batch 64, 22 x 257 (train.py:25,87; model.py:136-148), best of 1 and
-    16 threads.  Returns (cpu_baseline dict, real-loop dict)."""
+    """BASELINE.md section 3's CPU leg: the cfg2 step at B on 1 thread, on the box's per-GPU share (16)
+    and on every CPU of the affinity mask (torch.set_num_threads(len(os.sched_getaffinity(0)))), each
+    ``steps`` individually timed steps after one warm-up, trials/s at the median step; the headline is
+    the best leg.  Plus the reference's real loop at batch 64, 22 x 257 (train.py:25,87;
+    model.py:136-148) on 1 and 16 threads.  Returns (cpu_baseline dict, real-loop dict)."""
     affinity = len(os.sched_getaffinity(0))
     many = min(16, affinity)
     legs = {}
-    for th, st in ((many, steps), (1, 2)):
-        v, secs = cpu_baseline(B, C, T, st, th)
-        legs[th] = {"value": round(v, 1), "cores": th, "seconds": round(secs, 2), "steps": st}
+    for th in dict.fromkeys((1, many, affinity)):          # distinct thread counts, in this order
+        v, secs, times = cpu_baseline(B, C, T, steps, th)
+        legs[th] = {"value": round(v, 1), "cores": th, "seconds": round(secs, 2), "steps": steps,
+                    "median_step_s": round(float(np.median(times)), 3),
+                    "step_s": [round(t, 3) for t in times]}
     best = max(legs.values(), key=lambda e: e["value"])
     cpu = {"value": best["value"], "unit": "trials/s", "cores": best["cores"], "kind": "port",
-           "sample": f"train steps (fwd+CE+bwd+Adam) of B={B} x {C}x{T} after 1 warm-up: best of "
-                     f"{many} threads ({legs[many]['steps']} steps, {legs[many]['seconds']} s) and 1 thread "
-                     f"({legs[1]['steps']} steps, {legs[1]['seconds']} s); {affinity} CPUs in the affinity "
-                     f"mask, {many} = the box's share per GPU; torch {torch.__version__} CPU, "
-                     f"{cpu_model_name()}",
-           "legs": list(legs.values())}
+           "sample": f"train steps (fwd+CE+bwd+Adam) of B={B} x {C}x{T}: {steps} individually timed steps "
+                     f"per leg after 1 warm-up, trials/s at the median step, legs of "
+                     f"{', '.join(str(k) for k in legs)} threads ({affinity} CPUs in the affinity mask, "
+                     f"{many} = the box's share per GPU); the best leg is the value; torch "
+                     f"{torch.__version__} CPU (stock ATen, oracle/torch_ref.py)",
+           "legs": list(legs.values()), "host": host_cpu_info()}
     real = {}
-    for th in (many, 1):
-        v, secs = cpu_baseline(64, 22, 257, 40, th, real_loop=True)
+    for th in dict.fromkeys((many, 1)):
+        v, secs, _ = cpu_baseline(64, 22, 257, 40, th, real_loop=True)
         real[th] = {"value": round(v, 1), "cores": th, "seconds": round(secs, 2)}
     rb = max(real.values(), key=lambda e: e["value"])
     real_out = {"value": rb["value"], "unit": "trials/s", "cores": rb["cores"], "kind": "port",
                 "sample": "40 steps of the reference loop body (float64 batch -> .float(), forward, CE, "
                           ".item(), zero_grad, backward, Adam) at batch 64 x 22x257 after 1 warm-up, "
-                          f"best of {many} threads and 1 thread",
+                          f"trials/s at the median step, best of {many} threads and 1 thread",
                 "legs": list(real.values())}
     cpu["real_protocol_b64_t257"] = real_out
     return cpu, real_out
@@ -440,7 +464,45 @@ def bench_folds(dev, n_folds, n_train, epochs, rank=0, world=1, barrier=lambda: 
             [(FoldBatch([models[k]], [k], fused=False), [k]) for k in mine], epochs)
         out.update({"per_fold_streams_graphed_value": round(streams, 1),
                     "sequential_folds_value": round(alone, 1), "speedup": round(fused / alone, 2)})
+        if n_folds == 90:
+            out.update(fold_shares(dev, X, y, fused, fused_epochs))
     return out if rank == 0 else None
+
+
+def fold_shares(dev, X, y, rate90, epochs):
+    """cfg3's per-rank operating points on this one GPU: lpt_assign deals the 90 cross-subject folds
+    as 45 | 23, 22 | 12, 11 folds per rank at 2 / 4 / 8 GPUs, and each rank trains its share as one
+    fold batch (one launch per pass serves every resident fold), so the 8-GPU curve is set by the
+    fold launch's rate at 11-12 folds.  Times the fold-indexed, graphed epoch at each share (same data,
+    models seeded per fold) and predicts the n-GPU aggregate as 90 folds over the slowest rank's time
+    (the largest share; no communication).  Returns {"per_share": ..., "predicted_scaling": ...}."""
+    from eegnetreplication_amd import EEGNet, FoldBatch
+    from eegnetreplication_amd.distributed import lpt_assign
+    n_train = X.shape[0]
+    rates = {}
+    for k in (11, 12, 22, 23, 45):
+        torch.manual_seed(3)
+        fb = FoldBatch([EEGNet(22, 257, p=0.5).to(dev).train() for _ in range(k)], list(range(k)),
+                       graphs=True, fused=True)
+        gens = [torch.Generator().manual_seed(100 + j) for j in range(k)]
+        fb.epoch([(X, y)] * k, 64, gens)                      # warm-up (workspaces, graph capture)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(epochs):
+            fb.epoch([(X, y)] * k, 64, gens)
+        torch.cuda.synchronize()
+        rates[k] = k * n_train * epochs / (time.perf_counter() - t0)
+        del fb
+    rates[90] = rate90
+    pred = {}
+    for n in (1, 2, 4, 8):
+        share = max(len(r) for r in lpt_assign([1.0] * 90, n))
+        pred[str(n)] = round(90 * n_train / (share * n_train / rates[share]), 1)
+    return {"per_share": {str(k): round(v, 1) for k, v in sorted(rates.items())},
+            "predicted_scaling": pred,
+            "predicted_note": "n-GPU trials/s = 90 folds x 1,440 trials / the largest rank share's time at the "
+                              "per-share rate measured here (lpt_assign: 90 | 45 | 23 | 12 folds on the "
+                              "busiest rank at 1 / 2 / 4 / 8 GPUs); no data-path communication"}
 
 
 def bench_cfg4(dev, rank, world, G, steps, warmup, barrier, nx=2):
@@ -496,7 +558,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="trials per GPU per step")
     ap.add_argument("--C", type=int, default=22)
     ap.add_argument("--T", type=int, default=256)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-infer", action="store_true", help="skip the cfg5 bf16 inference leg")

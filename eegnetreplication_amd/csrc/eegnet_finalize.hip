@@ -440,14 +440,22 @@ __device__ __forceinline__ void adam_scalars_publish(const Geo& g, const FinArgs
     pub(fa.coef + CF_ADAM * CSTR, step_size);
     pub(fa.coef + CF_ADAM * CSTR + 1, bc2s);
 }
-__device__ void adam_slice(const Geo& g, const FinArgs& fa, int part, int nparts) {
+// step0: the device step counter as this workgroup read it BEFORE taking its reduction ticket.  fin5
+// (run by the ticket winner) advances *fa.step, and nothing orders a loser's later read against that
+// write: a loser descheduled past fin5 would apply the bias correction of the step after.  The wide
+// pass E calls this in its prologue (its finalize is a later launch), the narrow one passes the value
+// it read in its prologue.
+__device__ __forceinline__ int adam_step0(const Geo& g, const FinArgs& fa) {
+    return adam_early(g, fa) ? __builtin_amdgcn_readfirstlane(*fa.step) : 0;
+}
+__device__ void adam_slice(const Geo& g, const FinArgs& fa, int part, int nparts, int step0) {
     if (!adam_early(g, fa)) return;
     int i0, i1;
     adam_slice_range(g, part, nparts, i0, i1);
     const int i = i0 + (int)threadIdx.x;
     if (i0 + (int)(threadIdx.x & ~63u) >= i1) return;    // waves without an element (wave-uniform)
     float step_size, bc2s;
-    adam_scalars(fa, *fa.step + 1, step_size, bc2s);   // *fa.step: fin5 of this pass advances it later
+    adam_scalars(fa, step0 + 1, step_size, bc2s);
     for (int k = i; k < i1; k += (int)blockDim.x) {
         float pp = fa.params[k], mm = fa.adam_m[k], vv = fa.adam_v[k];
         adam_elem(&pp, fa.grads[k], &mm, &vv, fa.b1, fa.b2, step_size, bc2s, fa.eps);

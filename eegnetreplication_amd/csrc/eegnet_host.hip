@@ -87,9 +87,11 @@ static int grid_mult_cd() {
     return m;
 }
 
-// the compile-time shapes of the narrow passes (EEG_DISPATCH), whose x loads honour a row pitch
+// the compile-time shape of the narrow passes (EEG_DISPATCH) whose x loads honour a row pitch: 22 x 257
+// (the recordings), whose 257-float rows are not 16-byte units; 22 x 256 rows already are, and its
+// kernels take the pitch as the compile-time T (EEG_XP)
 static bool x_pitch_shape(const eegnet_dims& d) {
-    return d.K1 == 32 && d.C == 22 && (d.T == 256 || d.T == 257) && d.F1 == 8 && d.D == 2;
+    return d.K1 == 32 && d.C == 22 && d.T == 257 && d.F1 == 8 && d.D == 2;
 }
 
 static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
@@ -108,7 +110,7 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
         return fail(EEGNET_EINVAL, "T must be in [max(32,K1), 1024] (got %d)", g->T);
     g->XP = d->x_pitch ? d->x_pitch : g->T;
     if (g->XP != g->T && !(x_pitch_shape(*d) && (g->XP & 3) == 0 && g->XP > g->T))
-        return fail(EEGNET_EINVAL, "x_pitch %d: only the 22 x 256 / 257 EEGNet-8,2 (K1 = 32) training kernels take "
+        return fail(EEGNET_EINVAL, "x_pitch %d: only the 22 x 257 EEGNet-8,2 (K1 = 32) training kernels take "
                     "a row pitch, a multiple of 4 above T (eegnet_x_pitch)", g->XP);
     g->P = (g->K1 - 1) / 2; g->R = g->K1 - 1 - g->P;
     g->T1 = g->T / 4; g->T2 = g->T1 / 8; g->NF = g->F2 * g->T2;

@@ -27,6 +27,9 @@ constexpr int WPEB = NWB * WGPC / 4;   // waves per SIMD: HIP's __launch_bounds_
 // put octets oc and oc + 8 of one row in the same group: a 2-way conflict on every window read).
 __device__ __forceinline__ int fir_row(int lane) { return (lane >> 3) & 1; }
 __device__ __forceinline__ int fir_oct(int lane) { return (lane & 7) | ((lane >> 4) << 3); }
+// x row pitch: the compile-time shapes with T a multiple of 4 take contiguous rows only (make_geo), so
+// their pitch is the constant T -- no run-time stride or (XP & 3) branch in the DMA loops
+#define EEG_XP(TT, g) (((TT) && ((TT) & 3) == 0) ? (TT) : (g).XP)
 #define EEG_NO(TT) ((TT) ? ((TT) + 7) / 8 : ((T + 7) >> 3))
 #define EEG_MO(TT) ((TT) ? (((TT) + 7) / 8 + 31) / 32 : 4)
 
@@ -235,6 +238,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
                                                       FinArgs fa, FoldCall fc) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
+    const int XP = EEG_XP(TT, g);
     TRACE(g, 0, TR_ENTRY);
     const int64_t* perm = nullptr;                 // fold launches: trial rows through the permutation
     long long row0 = 0;
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     // compile-time shapes: the first trial's x goes out by LDS-DMA before anything else; the pad fill,
     // the weight loads and the edge decode below overlap it, and one barrier waits for all of it
     if constexpr (XDMA) {
-        if (b0 < b1) x_dma_asm(x + fold_row(perm, row0, b0) * (C * g.XP), C, T, g.XP, RS, LP, Xb, wave, lane);
+        if (b0 < b1) x_dma_asm(x + fold_row(perm, row0, b0) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
         zero_pads(sm, C + F2, RS, LP, T, tid);
     } else {
         zero_fill<false>(sm, (C + F2) * RS, C, RS, LP, T, tid);
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     if constexpr (XDMA) {
         barrier_vm<0>();                              // the first x landed, pads and tables written
     } else {
-        if (b0 < b1) x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * g.XP), C, T, pf, tid);
+        if (b0 < b1) x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * XP), C, T, pf, tid);
         __syncthreads();
         x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         __syncthreads();
@@ -367,8 +371,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         barrier_lds();                                     // Ss complete, x read for good (LDS only:
                                                            // the previous trial's v stores stay in flight)
         if (bn < b1) {                                     // next x: lands by the closing barrier
-            if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, bn) * (C * g.XP), C, T, g.XP, RS, LP, Xb, wave, lane);
-            else x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * g.XP), C, T, pf, tid);   // live over the FIR only
+            if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, bn) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
+            else x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * XP), C, T, pf, tid);   // live over the FIR only
         }
         TRACE_PH(g, 0, 1, tph_);
         // s rows -> the s plane [B][F2][T] (pass E's lag-correlation operand)
@@ -708,6 +712,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                                                       float* __restrict__ part, FinArgs fa, FoldCall fc) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
+    const int XP = EEG_XP(TT, g);
     TRACE(g, 4, TR_ENTRY);
     const int64_t* perm = nullptr;                 // fold launches: trial rows through the permutation
     long long row0 = 0;
@@ -849,12 +854,13 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         CT[tid] = src[o];
     }
     adam_scalars_publish(g, fa);
+    const int step0 = adam_step0(g, fa);           // before the reduction ticket (adam_slice)
     if constexpr (XDMA) barrier_vm<0>();          // first s / dp2 landed (asm DMA), pads and tables written
     else __syncthreads();
     if constexpr (!XDMA) {
         if (b0 < b1) {
             s_rows_put();
-            x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * g.XP), C, T, pfx, tid);
+            x_prefetch<PF, NTB>(x + fold_row(perm, row0, b0) * (C * XP), C, T, pfx, tid);
             x_store<PF, NTB>(pfx, C, T, RS, LP, Xb, tid);
         }
         __syncthreads();
@@ -922,7 +928,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         }
         // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
         // GEMM); they land during the lag correlation / FIR^T, by the next barrier
-        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * g.XP), C, T, g.XP, RS, LP, Xb, wave, lane);
+        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 2, tph_);
         {
             float tl[K1];
@@ -1074,7 +1080,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
             if constexpr (XDMA) s_dma_asm(sg + (size_t)bn * F2 * s_pitch(T), F2, T, RS, LP, Ss, wave, lane);
             else {                                         // registers over the dws GEMM only
                 s_rows_load(bn);
-                x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * g.XP), C, T, pfx, tid);
+                x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * XP), C, T, pfx, tid);
             }
             if constexpr (DPDMA) flat_dma_asm(dp2g + (size_t)bn * ndp, ndp, DP, wave, lane);
             asm volatile("" ::: "memory");                 // the v loads issue after the DMA (barrier_vm)
@@ -1199,7 +1205,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa, blockIdx.x);
         TRACE(g, 4, TR_FIN);
     } else {
-        adam_slice(g, fa, blockIdx.x, gridDim.x);  // off the critical path: the winner is still reducing
+        adam_slice(g, fa, blockIdx.x, gridDim.x, step0);  // off the critical path: the winner is still reducing
     }
 }
 

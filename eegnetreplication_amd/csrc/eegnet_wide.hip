@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         }
     };
     float vpf[MOW][8];
-    adam_slice(g, fa, blockIdx.x, gridDim.x);
+    adam_slice(g, fa, blockIdx.x, gridDim.x, adam_step0(g, fa));
     adam_scalars_publish(g, fa);
     __syncthreads();                                       // zero fill before the first rows land
     if (b0 < b1) { stage_rows(b0); vload(b0, vpf); }

@@ -172,11 +172,23 @@ class DataParallelTrainer:
                       lr=self.lr, betas=self.betas, eps=self.eps)
 
     # -- synchronised BatchNorm stages ----------------------------------------------------------
-    def stage(self, k, x, y, seed, offset):
+    def global_batch(self, B):
+        """The batch the synchronised statistics and the CE mean are normalised by: the sum of the
+        ranks' local batches, all-reduced every step (a short last batch on one rank -- a sampler with
+        drop_last=False -- must not mis-normalise every rank's statistics and gradients).  One small
+        collective and a host read per step, in the sync_bn path only."""
+        if self.world == 1:
+            return B
+        t = torch.tensor([B], dtype=torch.float64, device=self.model.flat_parameters().device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return int(t.item())
+
+    def stage(self, k, x, y, seed, offset, norm_batch=None):
         """eegnet_train_stage k (2j: pass j with its sums left in the workspace; 2j + 1: its finalize)."""
         m = self.model
         B = x.shape[0]
-        ops.train_stage(m.shape, k, B * self.world, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed,
+        nb = B * self.world if norm_batch is None else norm_batch
+        ops.train_stage(m.shape, k, nb, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed,
                         offset, self.adam.grads, self.adam.state, self.adam.step, self.workspace(B),
                         self.loss, lr=self.lr, betas=self.betas, eps=self.eps, nbt=m.flat_num_batches_tracked())
 
@@ -199,10 +211,11 @@ class DataParallelTrainer:
         seed = 0x5EED_0000 + self._step
         offset = self._step * self.world + self.rank
         sums = self.stage_sums(x.shape[0])
+        nb = self.global_batch(x.shape[0])
         for j in range(5):
-            self.stage(2 * j, x, y, seed, offset)
+            self.stage(2 * j, x, y, seed, offset, nb)
             self.reduce_sums(sums[j])
-            self.stage(2 * j + 1, x, y, seed, offset)
+            self.stage(2 * j + 1, x, y, seed, offset, nb)
         return self.loss
 
     def step(self, x, y):

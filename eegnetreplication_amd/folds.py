@@ -138,7 +138,9 @@ class FoldBatch:
               "copied": [None, None], "epoch": 0,
               "tables": {}, "steps": []}
         # x rows at the pitch the kernels load fastest (22 x 257: 260 floats, 16-byte DMA units):
-        # one padded copy per distinct X, kept for the life of this state
+        # one padded copy per distinct X, kept for the life of this state and refreshed in place
+        # (same storage: the tables and the graph stay valid) whenever X changes in place
+        # (X._version: a caller refilling a preallocated augmentation buffer)
         shape = self.models[0].shape
         xp = shape.x_pitch()
         st["x_pitch"] = 0 if xp == shape.T else xp
@@ -148,8 +150,8 @@ class FoldBatch:
             if ops.x_pitch_of(X) == st["x_pitch"]:
                 return X
             if id(X) not in st["xpad"]:
-                st["xpad"][id(X)] = ops.pad_x_rows(X, xp)
-            return st["xpad"][id(X)]
+                st["xpad"][id(X)] = [X, ops.pad_x_rows(X, xp), X._version]
+            return st["xpad"][id(X)][1]
         for j, i in enumerate(range(0, n, batch_size)):
             B = min(batch_size, n - i)
             st["steps"].append((i, j, B))
@@ -174,9 +176,20 @@ class FoldBatch:
             ops.train_step_folds(shape, B, st["tables"][B], K, row0=i, slot=j, offset=0, lr=self.lr,
                                  betas=self.betas, eps=self.eps, x_pitch=st["x_pitch"])
 
+    @staticmethod
+    def _refresh_padded(st):
+        """Re-copy every padded X whose source changed in place since it was padded."""
+        for ent in st["xpad"].values():
+            X, xpad, ver = ent
+            if X._version != ver:
+                with torch.no_grad():
+                    xpad.copy_(X)
+                ent[2] = X._version
+
     def _epoch_fused(self, data, batch_size, generators):
         n = data[0][0].shape[0]
         st = self._fused_state(data, batch_size)
+        self._refresh_padded(st)
         i = st["epoch"] & 1
         st["epoch"] += 1
         if st["copied"][i] is not None:     # this pinned buffer's copy (two epochs ago) has run

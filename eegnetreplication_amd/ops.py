@@ -111,7 +111,7 @@ def forward_train(shape: Shape, flat_params, bn_flat, x, ws, seed: int, offset: 
     B = x.shape[0]
     logits = torch.empty((B, NCLS), dtype=torch.float32, device=x.device)
     m2, m3 = masks if masks is not None else (None, None)
-    d = shape.dims(B, p)
+    d = shape.dims(B, p, x_pitch_of(x))
     _lib.check(_lib.load().eegnet_forward_train(
         ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(m2), _ptr(m3),
         ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(logits), _ptr(ws), _stream(),
@@ -129,7 +129,7 @@ def backward(shape: Shape, flat_params, x, ws, seed: int, offset: int, dlogits=N
     if grads is None:
         grads = torch.empty_like(flat_params)
     m2, m3 = masks if masks is not None else (None, None)
-    d = shape.dims(B, p)
+    d = shape.dims(B, p, x_pitch_of(x))
     _lib.check(_lib.load().eegnet_backward(
         ctypes.byref(d), _ptr(flat_params), _ptr(x), _ptr(dlogits), _ptr(labels), _ptr(m2),
         _ptr(m3), ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(loss), _ptr(ws),
@@ -144,6 +144,7 @@ def clamp_grads(shape: Shape, grads):
 
 
 def forward_eval(shape: Shape, flat_params, bn_flat, x) -> torch.Tensor:
+    x = x.contiguous()                # the eval kernels read [B][C][T] rows (no pitch)
     B = x.shape[0]
     logits = torch.empty((B, NCLS), dtype=torch.float32, device=x.device)
     d = shape.dims(B)
@@ -182,6 +183,9 @@ def x_pitch_of(x: torch.Tensor) -> int:
     B, C, T = x.shape
     if x.stride(2) != 1 or x.stride(0) != C * x.stride(1) or x.stride(1) < T:
         raise ValueError("x must be a contiguous [B, C, T] tensor or a [B, C, T] view of [B, C, pitch] rows")
+    if x.data_ptr() % 16:
+        # pitched rows go to LDS in 16-byte DMA units: every row must start 16-byte aligned
+        raise ValueError("a pitched x view must start 16-byte aligned")
     return int(x.stride(1))
 
 
@@ -218,7 +222,7 @@ def train_stage(shape: Shape, stage: int, norm_batch: int, flat_params, bn_flat,
     """eegnet_train_stage: stage 2k = pass k with its finalize deferred (sums left in ``ws``),
     stage 2k + 1 = pass k's finalize on the (all-reduced) sums; statistics normalised by
     ``norm_batch`` (the global batch of a synchronised-BatchNorm data-parallel step)."""
-    d = shape.dims(x.shape[0], p)
+    d = shape.dims(x.shape[0], p, x_pitch_of(x))
     _lib.check(_lib.load().eegnet_train_stage(
         ctypes.byref(d), ctypes.c_int(stage), ctypes.c_int64(norm_batch), _ptr(flat_params), _ptr(bn_flat),
         _ptr(x), _ptr(labels), ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),

@@ -147,16 +147,39 @@ def _device_fault(e: BaseException) -> bool:
     return isinstance(e, getattr(torch, "AcceleratorError", ())) or "HIP error" in msg or "CUDA error" in msg
 
 
+# host-side failures a fresh re-run can cure (I/O, data, host memory); programming errors (TypeError,
+# AttributeError, ...) and device faults are not retried
+RETRYABLE = (OSError, ValueError, KeyError, IndexError, MemoryError, RuntimeError)
+
+
+def _device_usable() -> bool:
+    """After a failed unit: no stream left in graph capture and the device still synchronises (a
+    failure inside torch.cuda.graph capture can leave the stream capturing or invalidated; a re-run
+    on it would fail with an unrelated error)."""
+    if not torch.cuda.is_available():
+        return True
+    try:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        torch.cuda.synchronize()
+    except Exception:                                # noqa: BLE001 -- any failure: not usable
+        return False
+    return True
+
+
 def _with_retry(fn, what, retries=None):
     """Run one idempotent unit (a fold, or a batch of folds), re-running it from a fresh state if a
     host-side exception escapes (a fold is an idempotent unit).  Every unit builds its
-    model, generator and loaders from its own seed, so a re-run reproduces the result bit for bit."""
+    model, generator and loaders from its own seed, so a re-run reproduces the result bit for bit.
+    Only RETRYABLE exceptions that are not device faults are re-run, and only on a device that is
+    out of graph capture and still synchronises."""
     retries = UNIT_RETRIES if retries is None else retries
     for attempt in range(retries + 1):
         try:
             return fn()
         except Exception as e:                       # noqa: BLE001 -- re-raised below
-            if attempt == retries or _device_fault(e):
+            if (attempt == retries or _device_fault(e) or not isinstance(e, RETRYABLE)
+                    or not _device_usable()):
                 raise
             logger.warning(f"{what} failed ({e!r}); re-running it from a fresh state "
                            f"(attempt {attempt + 2}/{retries + 1})")
@@ -252,10 +275,13 @@ def cross_subject_units():
     return units
 
 
-def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0, max_units=None):
+def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0, max_units=None,
+                           units_out=None):
     """train.py:151-291.  Returns (best_model_state, per_subject_test_acc, avg_test_acc).
     ``fold_batch`` > 1 trains that many of this rank's folds together (FoldBatch).
-    ``max_units`` restricts the run to the first folds (subjects with no fold are left out)."""
+    ``max_units`` restricts the run to the first folds (subjects with no fold are left out).
+    ``units_out``: a dict that receives every fold's merged result (fold index -> test / validation
+    accuracy, validation loss, final state), on every rank."""
     rank, world, _ = D.env_rank_world()
     units = cross_subject_units()
     mine = _select(units, max_units, world, rank)
@@ -279,6 +305,8 @@ def cross_subject_training(epochs=EPOCHS, seed=0, device="cuda", fold_batch=0, m
     for u, r in zip(mine, _run_units(specs, epochs, device, fold_batch)):
         local[u] = r
     res = D.gather_results(local)
+    if units_out is not None:
+        units_out.update(res)
     per_subject, all_acc = [], []
     best_loss, best_state = 100, None
     for s in range(1, N_SUBJECTS + 1):

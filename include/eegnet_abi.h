@@ -204,7 +204,9 @@ size_t eegnet_trace_bytes(void);
 /* The x row pitch the training entry points (eegnet_train_step, _folds, _forward_train, _backward,
  * _train_stage) load fastest for `dims`: T rounded up to 4 floats when the kernels for these dims take
  * x rows in 16-byte units at such a pitch (22 x 257, the recordings' shape: a 257-float row is not
- * 16-byte aligned), else T.  Every other entry point needs x_pitch = 0 or T.  No GPU needed. */
+ * 16-byte aligned), else T.  Only those dims accept a pitch other than T (22 x 256 rows are 16-byte
+ * units already; its kernels have the pitch T compiled in).  Every other entry point needs x_pitch = 0
+ * or T.  No GPU needed. */
 int eegnet_x_pitch(const eegnet_dims* dims);
 
 /* 1 when `dims` run the wide kernels compiled for the EEGNet-16,4 64 x 512 geometry (compile-time

@@ -140,3 +140,5 @@ def test_x_pitch_entry_point_and_validation():
     assert ok(_lib.dims(64, 22, 257, x_pitch=258)) != 0          # not a multiple of 4
     assert ok(_lib.dims(64, 22, 257, x_pitch=256)) != 0          # below T
     assert ok(_lib.dims(64, 32, 257, x_pitch=260)) != 0          # a runtime-shape kernel
+    assert ok(_lib.dims(64, 22, 256, x_pitch=256)) == 0
+    assert ok(_lib.dims(64, 22, 256, x_pitch=260)) != 0          # 22 x 256: pitch compiled in as T

@@ -160,16 +160,17 @@ def _syncbn_worker(rank, world, port, q):
     tr.stage_sums = lambda B: sums
     seen = []
 
-    def stage(k, x, y, seed, offset):
+    def stage(k, x, y, seed, offset, norm_batch):
         j = k // 2
         if k % 2 == 0:
             sums[j].copy_(torch.arange(sums[j].numel(), dtype=torch.float64) * (rank + 1) + 100 * j)
-            seen.append(("pass", j, seed, offset))
+            seen.append(("pass", j, seed, offset, norm_batch))
         else:
-            seen.append(("fin", j, sums[j].clone().numpy()))
+            seen.append(("fin", j, sums[j].clone().numpy(), norm_batch))
 
     tr.stage = stage
-    tr.step(torch.zeros(8, 22, 256), torch.zeros(8, dtype=torch.int64))
+    B = 8 - 3 * rank                      # unequal shards (a short last batch on rank 1)
+    tr.step(torch.zeros(B, 22, 256), torch.zeros(B, dtype=torch.int64))
     q.put((rank, seen))
     dist.destroy_process_group()
 
@@ -198,3 +199,5 @@ def test_sync_bn_step_reduces_every_pass_before_its_finalize():
     p0 = [e for e in res[0][1] if e[0] == "pass"][0]
     p1 = [e for e in res[1][1] if e[0] == "pass"][0]
     assert p0[2] == p1[2] and p0[3] != p1[3]
+    # every stage of every rank normalises by the true global batch 8 + 5, not local B x world
+    assert {e[-1] for _, seen in res for e in seen} == {13}

@@ -269,3 +269,33 @@ def test_padded_x_rows_bit_identical(B):
                      torch.cat(losses)))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_in_place_x_update_is_seen_by_the_padded_fold_launch():
+    """22 x 257 fold launches train from a padded copy of each fold's X (FoldBatch._fused_state).  A
+    caller that refills X in place between epochs (a preallocated augmentation buffer) must train on
+    the new values: graphed fold launches over an X mutated in place equal, bit for bit, the same
+    folds trained on a fresh tensor holding the new values."""
+    from eegnetreplication_amd import FoldBatch
+    dev = _dev()
+    X0, y = _data(192, 31, dev)
+    X1, _ = _data(192, 32, dev)
+    runs = []
+    for mode in ("in_place", "fresh"):
+        models = _models(2, 0.5, dev)
+        fb = FoldBatch(models, [5, 6], graphs=True, fused=True)
+        gens = [torch.Generator().manual_seed(s) for s in (5, 6)]
+        X = X0.clone()
+        fb.epoch([(X, y)] * 2, 64, gens)             # eager epoch on X0 (pads, captures)
+        if mode == "in_place":
+            X.copy_(X1)                              # same tensor, new values
+            Xe = X
+        else:
+            Xe = X1.clone()                          # a new tensor: new state, new padded copy
+        fb.epoch([(Xe, y)] * 2, 64, gens)
+        fb.epoch([(Xe, y)] * 2, 64, gens)
+        torch.cuda.synchronize()
+        runs.append([_state(fb, k) for k in range(2)])
+    for k in range(2):
+        for a, b in zip(runs[0][k], runs[1][k]):
+            assert torch.equal(a, b), f"fold {k}: the in-place update of X was not seen"

@@ -73,29 +73,43 @@ def test_eval_logits_match_reference():
 
 @pytest.mark.parametrize("name", ["G1", "G5_B1", "G5_8x64"])
 def test_fused_train_step_matches_reference(name):
-    """eegnet_train_step (forward + CE + backward + clamps + Adam in one device sequence)."""
+    """eegnet_train_step (forward + CE + backward + clamps + Adam in one device sequence).  p = 0
+    fixtures: against the reference's own vectors.  G5_8x64 (p = 0.25, a run-time 8 x 64 shape): the
+    fused step draws its masks on the device, so the expected values are the float64 oracle's step
+    from the fixture's (reference-generated) initial state given the masks the restated device
+    generator draws for the step's (seed, offset) (tests/hip_cases.py device_masks)."""
     from eegnetreplication_amd import FusedTrainer
+    from oracle import numpy_ref as nr
+    from hip_cases import device_masks
     dev = _dev()
     g = Golden(name)
-    if g.meta["p"] != 0:
-        pytest.skip("fused path draws masks on device")
+    m = g.meta
     model = _model_from(g, dev).train()
+    if m["p"] != 0:
+        seed, offset = 0x0DD5_EED5, 3
+        model.next_dropout_key = lambda: (seed, offset)
+        masks = device_masks(m["B"], m["F1"] * m["D"], m["T"], seed, offset, m["p"])
+        st = nr.adam_init(g.init_params())
+        ref = nr.train_step(g.init_params(), g.init_buffers(), g.x, g.y, st, p=m["p"], masks=masks)
+        exp_logits, exp_loss, exp_grads, exp_step1 = ref["logits"], ref["loss"], ref["grads"], ref["params"]
+    else:
+        exp_logits, exp_loss = g.z["logits"], float(g.z["loss"])
+        exp_grads, exp_step1 = g.group("grad"), g.group("step1")
     tr = FusedTrainer(model, lr=1e-3, eps=1e-7)
     x = torch.from_numpy(g.x).to(dev)
     y = torch.from_numpy(g.y).to(dev)
     logits = torch.empty((x.shape[0], 4), device=dev)
     loss = tr.step(x, y, logits=logits)
-    assert_close(logits.cpu().numpy(), g.z["logits"], name="logits")
-    assert abs(float(loss) - float(g.z["loss"])) <= 1e-4 * max(1.0, abs(float(g.z["loss"])))
-    from eegnetreplication_amd.ops import Shape  # noqa: F401
+    assert_close(logits.cpu().numpy(), exp_logits, name="logits")
+    assert abs(float(loss) - float(exp_loss)) <= 1e-4 * max(1.0, abs(float(exp_loss)))
     n = 0
     gr = {}
     for k, p in model.named_parameters():
         gr[k] = tr.adam.grads[n:n + p.numel()].view(p.shape).cpu().numpy()
         n += p.numel()
-    assert_grads_close(gr, g.group("grad"), prefix="grad.")
+    assert_grads_close(gr, exp_grads, prefix="grad.")
     assert_params_close({k: p.detach().cpu().numpy() for k, p in model.named_parameters()},
-                        g.group("step1"), prefix="step1.")
+                        exp_step1, prefix="step1.")
 
 
 def test_fused_trajectory_G7():

@@ -50,9 +50,12 @@ def _run(protocol, max_units):
     T_ = importlib.import_module("eegnetreplication_amd.train")    # (the package exports train())
     if protocol == "ws":
         per_subject, avg, states = T_.within_subject_training(EPOCHS, 0, "cuda:0", 90, max_units)
-        return per_subject, avg, [_np_state(s) for s in states]
-    best, per_subject, avg = T_.cross_subject_training(EPOCHS, 0, "cuda:0", 90, max_units)
-    return per_subject, avg, [_np_state(best)]
+        return per_subject, avg, [_np_state(s) for s in states], {}
+    units = {}
+    best, per_subject, avg = T_.cross_subject_training(EPOCHS, 0, "cuda:0", 90, max_units, units_out=units)
+    # every fold's record: test / validation accuracy, validation loss and its final state
+    per_fold = {u: (r["test_acc"], r["val_acc"], r["val_loss"], _np_state(r["state"])) for u, r in units.items()}
+    return per_subject, avg, [_np_state(best)], per_fold
 
 
 def _worker(rank, world, port, protocol, max_units, data_dir, q):
@@ -81,7 +84,7 @@ def _sharded(protocol, max_units, data_dir, world=2):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=110) for _ in range(world)], key=lambda r: r[0])
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
     for r in res:
@@ -91,7 +94,9 @@ def _sharded(protocol, max_units, data_dir, world=2):
     return res
 
 
-@pytest.mark.parametrize("protocol,max_units", [("ws", 18), ("cs", 12)])
+# ("cs", None): BASELINE configs[2] at its own size -- all 90 cross-subject folds, dealt 45 + 45 over
+# the two ranks (one launch of 90 folds at world 1 against two of 45)
+@pytest.mark.parametrize("protocol,max_units", [("ws", 18), ("cs", 12), ("cs", None)])
 def test_sharded_protocol_equals_world1(tmp_path, monkeypatch, protocol, max_units):
     _dev()
     data_dir = str(tmp_path / "nodata")
@@ -109,6 +114,14 @@ def test_sharded_protocol_equals_world1(tmp_path, monkeypatch, protocol, max_uni
             assert sorted(sa) == sorted(sb)
             for k in sb:
                 np.testing.assert_array_equal(sa[k], sb[k], err_msg=f"rank {rank} {protocol}: {k}")
+        assert sorted(got[3]) == sorted(one[3])
+        if max_units is None and protocol == "cs":
+            assert len(one[3]) == 90
+        for u, (ta, va, vl, st) in one[3].items():
+            tb, vb, wl, sb = got[3][u]
+            assert (ta, va, vl) == (tb, vb, wl), f"rank {rank} fold {u}: accuracies / validation loss differ"
+            for k in st:
+                np.testing.assert_array_equal(sb[k], st[k], err_msg=f"rank {rank} fold {u}: {k}")
 
 
 def test_fold_result_independent_of_fold_batch_width():

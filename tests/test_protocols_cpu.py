@@ -209,3 +209,36 @@ def test_failed_unit_is_retried_from_a_fresh_state(monkeypatch):
     monkeypatch.setattr(T_, "_run_folds", gpu_fault)
     with pytest.raises(RuntimeError, match="HIP error"):
         T_._run_units(specs, 1, "cpu", fold_batch=3)
+
+
+def test_retry_only_host_failures_on_a_usable_device(monkeypatch):
+    """A programming error (TypeError) is not retried, and neither is any failure after which the
+    device is unusable (a stream left in graph capture, a failing synchronise)."""
+    import pytest
+    import importlib
+    T_ = importlib.import_module("eegnetreplication_amd.train")
+    calls = {"n": 0}
+
+    def bug():
+        calls["n"] += 1
+        raise TypeError("a bug, not a host-side failure")
+
+    with pytest.raises(TypeError):
+        T_._with_retry(bug, "unit")
+    assert calls["n"] == 1
+
+    calls["n"] = 0
+
+    def io_then_ok():
+        calls["n"] += 1
+        if calls["n"] == 1:
+            raise OSError("injected I/O failure")
+        return "ok"
+
+    assert T_._with_retry(io_then_ok, "unit") == "ok" and calls["n"] == 2
+
+    calls["n"] = 0
+    monkeypatch.setattr(T_, "_device_usable", lambda: False)
+    with pytest.raises(OSError):
+        T_._with_retry(io_then_ok, "unit")
+    assert calls["n"] == 1
