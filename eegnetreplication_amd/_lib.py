@@ -21,7 +21,8 @@ _lib = None
 class Fold(ctypes.Structure):
     """Mirror of ``eegnet_fold`` (include/eegnet_abi.h): one model of a fold-indexed step."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("params", "bn_buffers", "num_batches_tracked", "x", "labels",
-                                              "grads", "adam_state", "step", "losses", "ws", "perm")] + \
+                                              "grads", "adam_state", "step", "losses", "ws", "perm",
+                                              "xstat")] + \
                [("seed", ctypes.c_uint64)]
 
 
@@ -69,6 +70,8 @@ _SIGS = {
     "eegnet_dims_bytes": (ctypes.c_size_t, []),
     "eegnet_wide_spec": (ctypes.c_int, [ctypes.POINTER(Dims)]),
     "eegnet_x_pitch": (ctypes.c_int, [ctypes.POINTER(Dims)]),
+    "eegnet_x_stats_width": (ctypes.c_int, [ctypes.POINTER(Dims)]),
+    "eegnet_x_stats": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.c_int64, _vp, _vp, _vp]),
     "eegnet_fold_bytes": (ctypes.c_size_t, []),
     "eegnet_last_error": (ctypes.c_char_p, []),
     "eegnet_build_info": (ctypes.c_char_p, []),

@@ -91,7 +91,7 @@ struct Geo {
     X(o_Wfc, 10016) X(o_bfc, 14112) X(nparam, 14116) X(nA, 448) X(nB, 128) X(nC, 4229) X(nD, 5248)    \
     X(nE, 6272) X(QR, 64) X(wide, 1) X(NOC, 4) X(CPC, 16) X(F2P, 64) X(RB, 144) X(splitC, 1)         \
     X(splitD, 1) X(splitE, 1) X(ldsWA, 19120) X(ldsWB, 0) X(ldsWB2, 23872) X(ldsWC, 10528)           \
-    X(ldsWD, 37952) X(ldsWE, 21736) X(ldsWI, 37760)
+    X(ldsWD, 37952) X(ldsWE, 20736) X(ldsWI, 37760)
 __host__ __device__ __forceinline__ void shape_w5(Geo& g) {
 #define EEG_SET_(f, v) g.f = v;
     EEG_SHAPE_W5(EEG_SET_)
@@ -192,7 +192,7 @@ constexpr int TK_PASSES = 5;      // ticket blocks: passes A..E, contiguous from
 struct FinArgs {
     double* part2;                // [ngrp][ncols] fp64 group partials
     unsigned* cnt;                // this pass's NCNT ticket words
-    double* stats;                // lag-Gram + window sums (fin1 writes, fin5 reads)
+    double* stats;                // G w1 per filter + window sums S1 (fin1 writes, fin5 reads)
     float* coef;
     float* bn;                    // running statistics (fin1/fin2, when update_running)
     float* grads;

@@ -198,18 +198,26 @@ __device__ __forceinline__ void bn_running(float* rm, float* rv, double mu, doub
 // (a finalize runs on the critical path between two launches: every dependent global round trip
 // there is a few hundred ns with the rest of the GPU idle)
 __host__ __device__ constexpr int fin1_scratch_doubles(int K1, int F1, int F2, int C) {
-    return K1 * K1 + K1 + 128 + (F1 * K1 + 2 * F1 + F2 * C + 2 * F1 + 2 * F2 + 1) / 2 + 2;
+    // G [K1][K1+1] | S1 | a1, c1 [64 each] | staged floats | G w1 products [2][F1 K1]
+    return K1 * (K1 + 1) + K1 + 128 + (F1 * K1 + 2 * F1 + F2 * C + 2 * F1 + 2 * F2 + 3) / 2 + 2 * F1 * K1 + 2;
 }
 // (ng = the number of leading parameters fin5 itself differentiates: o_g2)
 __host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1, int ng) {
-    return K1 * K1 + K1 + 128 + F1 * K1 + (CF_COUNT * CSTR + ng + 1) / 2 + 2;
+    // G w1 [F1 K1] | S1 [K1] | db1, dg1 [64 each] | coefficient block | gradients [0, ng) (floats)
+    return F1 * K1 + K1 + 128 + (CF_COUNT * CSTR + ng + 1) / 2 + 2;
 }
 
-// after pass A: BN1 (model.py:32) and BN2 (model.py:47) batch statistics
+// after pass A: BN1 (model.py:32) and BN2 (model.py:47) batch statistics.  Latency is what matters
+// here (one workgroup on the critical path between two launches), so every dependent step is short:
+// the lag-Gram's edge differences Ed[d][j] in parallel, one serial prefix per lag d (a lane each), the
+// matrix-vector products G w1 as (filter, tap) lanes with four partial chains, and the filters' sums
+// over taps from LDS -- no shuffle scans.  G w1 and S1 go to fa.stats for fin5 (dW1 needs exactly those,
+// the same parameters being in force through pass E).
 __device__ void fin1(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
     const int K1 = g.K1, F1 = g.F1, F2 = g.F2, C = g.C, nth = blockDim.x;
-    double* Gm = scr;                 // K1*K1
-    double* S1 = Gm + K1 * K1;        // K1
+    const int GS = K1 + 1;            // padded row stride of G and Ed (conflict-free column walks)
+    double* Gm = scr;                 // K1 * GS
+    double* S1 = Gm + K1 * GS;        // K1
     double* a1s = S1 + K1;            // F1 (<= 64)
     double* c1s = a1s + 64;
     // staged global inputs (floats): w1 | g1 | b1 | ws | rm1 rv1 | rm2 rv2
@@ -219,6 +227,9 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     float* pb1 = pg1 + F1;
     float* pws = pb1 + F1;
     float* pbn = pws + F2 * C;
+    // after the staged floats: the per-(filter, tap) products [2][F1 K1]
+    double* pq = (double*)(pl + ((F1 * K1 + 2 * F1 + F2 * C + 2 * F1 + 2 * F2 + 3) & ~1));
+    double* pm = pq + F1 * K1;
     const int tid = threadIdx.x;
     {   // w1 | g1 | b1 | ws are contiguous in the parameter vector (eegnet_host.hip param layout)
         const int nl = F1 * K1 + 2 * F1 + F2 * C, nb = 2 * F1 + 2 * F2;
@@ -240,74 +251,82 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     const double* Sv2 = Sv + F2;
     // lag-Gram of the padded rows: G[k][k+d] = G0[d] + sum_{j<k} Ed[d][j], with
     // Ed[d][j] = sum_c X[T+j]X[T+j+d] - X[j]X[j+d] = Tl[j][j+d] (j+d < P) - H[j-P][j-P+d] (j >= P).
-    // One K1-lane segment per lag d (K1 | 64: segments never straddle a wave), prefix sums by
-    // shuffle scan: no serial chain over k.
-    for (int t = tid; t < K1 * K1; t += nth) {
-        const int d = t / K1, j = t - d * K1;
+    // Lag d is one lane's serial prefix over k (its loads do not depend on the chain: unrolled, they
+    // issue ahead of the adds).
+    if (tid < K1) {
+        const int d = tid;
+        const double base = G0[d];
         double e = 0.0;
-        if (j < K1 - 1 - d) {
-            if (j + d < g.P) e += Tl[j * g.P - j * (j - 1) / 2 + d];
-            if (j >= g.P) {
-                const int a = j - g.P;
-                e -= H[a * g.R - a * (a - 1) / 2 + d];
+#pragma unroll 8
+        for (int k = 0; k < K1; ++k) {
+            if (k + d < K1) {
+                const double v = base + e;
+                Gm[k * GS + k + d] = v;
+                Gm[(k + d) * GS + k] = v;
+                double ed = 0.0;
+                if (k < K1 - 1 - d) {
+                    if (k + d < g.P) ed += Tl[k * g.P - k * (k - 1) / 2 + d];
+                    if (k >= g.P) {
+                        const int a = k - g.P;
+                        ed -= H[a * g.R - a * (a - 1) / 2 + d];
+                    }
+                }
+                e += ed;
             }
         }
-        for (int o = 1; o < K1; o <<= 1) {
-            const double y = __shfl_up(e, o, K1);
-            if (j >= o) e += y;
+    } else if (tid == 64) {           // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j])
+        double e = 0.0;
+        for (int k = 0; k < K1; ++k) {
+            S1[k] = S0 + e;
+            e += (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
         }
-        const double base = G0[d];
-        if (j == 0) { Gm[d] = base; Gm[d * K1] = base; }            // k = 0
-        const int k = j + 1;                                        // inclusive(j) = sum_{j' < k}
-        if (k + d < K1) {
-            const double v = base + e;
-            Gm[k * K1 + k + d] = v;
-            Gm[(k + d) * K1 + k] = v;
-        }
-    }
-    if (tid < 64) {       // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j]), same scan
-        const int k = tid;
-        double e = k < K1 - 1 ? (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0) : 0.0;
-        const double own = e;
-        for (int o = 1; o < 64; o <<= 1) {
-            const double y = __shfl_up(e, o, 64);
-            if (k >= o) e += y;
-        }
-        if (k < K1) S1[k] = S0 + (e - own);
     }
     __syncthreads();
     TRACE_FS(g, fa.tpass, 4);
-    for (int i = tid; i < K1 * K1 + K1; i += nth) fa.stats[i] = Gm[i];
-    // BN1 moments from the quadratic forms w^T G w and w^T S1: one (filter, tap) per lane, the
-    // filter's K1 lanes reduced by shuffles (G symmetric: column reads)
-    const double n1 = (double)g.Bn * C * g.T;
+    // G w1 per (filter, tap): row k of the symmetric G, four partial chains
     for (int p = tid; p < F1 * K1; p += nth) {
         const int gg = p / K1, k = p - gg * K1;
         const float* w = pw1 + gg * K1;
-        double r = 0.0;
-        for (int l = 0; l < K1; ++l) r += Gm[l * K1 + k] * (double)w[l];
-        const double wk = (double)w[k];
-        double q = wk * r, m = wk * S1[k];
-        for (int o = K1 / 2; o > 0; o >>= 1) {
-            q += __shfl_xor(q, o, K1);
-            m += __shfl_xor(m, o, K1);
+        const double* gr = Gm + k * GS;
+        double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0;
+        for (int l = 0; l < K1; l += 4) {
+            r0 += gr[l] * (double)w[l];
+            r1 += gr[l + 1] * (double)w[l + 1];
+            r2 += gr[l + 2] * (double)w[l + 2];
+            r3 += gr[l + 3] * (double)w[l + 3];
         }
-        if (k == 0) {
-            const double mu = m / n1;
-            const double var = fmax(q / n1 - mu * mu, 0.0);   // E[u^2] - mu^2: never below 0
-            const double inv = 1.0 / sqrt(var + (double)g.eps);
-            const double a1 = (double)pg1[gg] * inv;
-            const double c1 = (double)pb1[gg] - a1 * mu;
-            a1s[gg] = a1; c1s[gg] = c1;
-            fa.coef[CF_A1 * CSTR + gg] = (float)a1;
-            fa.coef[CF_C1 * CSTR + gg] = (float)c1;
-            fa.coef[CF_INV1 * CSTR + gg] = (float)inv;
-            fa.coef[CF_MU1 * CSTR + gg] = (float)mu;
-            if (fa.update_running) {
-                const double mom = g.mom;
-                fa.bn[gg] = (float)((1.0 - mom) * (double)pbn[gg] + mom * mu);
-                fa.bn[F1 + gg] = (float)((1.0 - mom) * (double)pbn[F1 + gg] + mom * var * n1 / (n1 - 1.0));
-            }
+        const double r = (r0 + r1) + (r2 + r3);
+        const double wk = (double)w[k];
+        pq[p] = wk * r;
+        pm[p] = wk * S1[k];
+        fa.stats[p] = r;                                   // fin5: (G w1)[k]
+        if (gg == 0) fa.stats[F1 * K1 + k] = S1[k];        // fin5: S1[k]
+    }
+    __syncthreads();
+    // BN1 moments from the quadratic forms w^T G w and w^T S1 (a filter per thread)
+    const double n1 = (double)g.Bn * C * g.T;
+    if (tid < F1) {
+        const int gg = tid;
+        double q0 = 0.0, q1 = 0.0, m0 = 0.0, m1 = 0.0;
+        for (int k = 0; k < K1; k += 2) {
+            q0 += pq[gg * K1 + k]; q1 += pq[gg * K1 + k + 1];
+            m0 += pm[gg * K1 + k]; m1 += pm[gg * K1 + k + 1];
+        }
+        const double q = q0 + q1, m = m0 + m1;
+        const double mu = m / n1;
+        const double var = fmax(q / n1 - mu * mu, 0.0);   // E[u^2] - mu^2: never below 0
+        const double inv = 1.0 / sqrt(var + (double)g.eps);
+        const double a1 = (double)pg1[gg] * inv;
+        const double c1 = (double)pb1[gg] - a1 * mu;
+        a1s[gg] = a1; c1s[gg] = c1;
+        fa.coef[CF_A1 * CSTR + gg] = (float)a1;
+        fa.coef[CF_C1 * CSTR + gg] = (float)c1;
+        fa.coef[CF_INV1 * CSTR + gg] = (float)inv;
+        fa.coef[CF_MU1 * CSTR + gg] = (float)mu;
+        if (fa.update_running) {
+            const double mom = g.mom;
+            fa.bn[gg] = (float)((1.0 - mom) * (double)pbn[gg] + mom * mu);
+            fa.bn[F1 + gg] = (float)((1.0 - mom) * (double)pbn[F1 + gg] + mom * var * n1 / (n1 - 1.0));
         }
     }
     __syncthreads();
@@ -469,12 +488,11 @@ constexpr int APT = 8;            // Adam elements per finalize thread: nparam <
 __device__ void fin5(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa,
                      int own_slice = -1) {
     const int tid = threadIdx.x, nth = blockDim.x, K1 = g.K1, F1 = g.F1;
-    double* Gm = scr;                 // K1*K1 (+ S1 K1), from fa.stats
-    double* S1 = Gm + K1 * K1;
+    double* Gw = scr;                 // (G w1)[filter][tap] (F1*K1) + S1 (K1), fin1's, from fa.stats
+    double* S1 = Gw + F1 * K1;
     double* db1s = S1 + K1;           // 64
     double* dg1s = db1s + 64;         // 64
-    double* wd = dg1s + 64;           // F1*K1
-    float* cf = (float*)(wd + F1 * K1);          // coefficient block [CF_COUNT][CSTR]
+    float* cf = (float*)(dg1s + 64);             // coefficient block [CF_COUNT][CSTR]
     float* gL = cf + CF_COUNT * CSTR;            // [0, o_g2): the gradients this finalize computes
     const double* Q = sums;
     const double* Xm = sums + g.QR * K1;
@@ -493,10 +511,8 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     float es0 = 0.f, es1 = 0.f;
     {
         Stage<3, double> s0;
-        Stage<1, float> s1;
         Stage<3, float> s2;
-        s0.load(fa.stats, K1 * K1 + K1);
-        s1.load(prm + g.o_w1, F1 * K1);
+        s0.load(fa.stats, F1 * K1 + K1);
         s2.load(fa.coef, CF_COUNT * CSTR);
         if (adam) {   // parameters, moments and the earlier finalizes' gradients (indices >= o_g2)
             const int last = ne - 1;
@@ -512,8 +528,7 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
             es0 = ld_pub(fa.coef + CF_ADAM * CSTR);
             es1 = ld_pub(fa.coef + CF_ADAM * CSTR + 1);
         }
-        s0.store(Gm, K1 * K1 + K1);
-        s1.store(wd, F1 * K1);
+        s0.store(Gw, F1 * K1 + K1);
         s2.store(cf, CF_COUNT * CSTR);
     }
     __syncthreads();
@@ -545,12 +560,10 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     const double n1 = (double)g.Bn * g.C * g.T;
     for (int p = tid; p < F1 * K1; p += nth) {
         const int gg = p / K1, k = p - gg * K1;
-        const double* w = wd + gg * K1;
         double qg = 0.0;
         if (g.QR == F1) qg = Q[gg * K1 + k];           // rows of a group summed in pass E
         else for (int o = gg * g.D; o < (gg + 1) * g.D; ++o) qg += Q[o * K1 + k];
-        double ux = 0.0;
-        for (int l = 0; l < K1; ++l) ux += w[l] * Gm[l * K1 + k];
+        const double ux = Gw[p];                       // (G w1)[k], fin1's (same w1: Adam runs after)
         const double inv1 = cf[CF_INV1 * CSTR + gg], mu1 = cf[CF_MU1 * CSTR + gg];
         const double xhx = inv1 * (ux - mu1 * S1[k]);
         const double a1 = cf[CF_A1 * CSTR + gg];

@@ -249,7 +249,7 @@ static WsLayout make_layout(const Geo& g) {
     L.partE = take((size_t)g.gridS * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
     L.sums = take((size_t)nmax * 8 * NGRPMAX);
-    L.stats = take((size_t)(g.K1 * g.K1 + g.K1) * 8);
+    L.stats = take((size_t)(g.F1 * g.K1 + g.K1) * 8);   // fin1 -> fin5: G w1 per filter, window sums S1
     L.coef = take((size_t)CF_COUNT * CSTR * 4);
     const size_t per = (size_t)g.B * g.F2 * g.T1 * 4;
     L.d2 = take(per); L.E1 = take(per); L.E2 = take(per); L.dp2 = take(per);
@@ -358,6 +358,8 @@ static void ensure_attrs() {
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 0, 0, 0>();
     set_attrs_shape<64, 0, 0, 0>();
+    hipFuncSetAttribute((const void*)k_xstats<32>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    hipFuncSetAttribute((const void*)k_xstats<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 22, 256, 16>();
     set_attrs_shape<32, 22, 257, 16>();
     g_attr_done = true;
@@ -1001,6 +1003,31 @@ int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fo
                            mode, &adam, s, fc, nfolds)
         : run_backward<64>(g, L, w, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                            mode, &adam, s, fc, nfolds);
+}
+
+int eegnet_x_stats_width(const eegnet_dims* dims) {
+    Geo g;
+    if (int r = make_geo(dims, &g, false)) return r;
+    if (g.wide) return fail(EEGNET_EINVAL, "eegnet_x_stats: F1*D = %d > 16 is not supported", g.F2);
+    return g.K1 + 1 + g.nedge;
+}
+
+int eegnet_x_stats(const eegnet_dims* dims, int64_t n, const float* x, float* out, void* stream) {
+    Geo g;
+    if (int r = make_geo(dims, &g)) return r;
+    if (g.wide) return fail(EEGNET_EINVAL, "eegnet_x_stats: F1*D = %d > 16 is not supported", g.F2);
+    if (n < 0) return fail(EEGNET_EINVAL, "n must be >= 0");
+    if (n == 0) return 0;
+    if (int r = check_ptrs(x, "x", out, "out")) return r;
+    ensure_attrs();
+    const size_t lds = (size_t)(g.C * g.RS + NWB * (g.K1 + 1)) * 4;
+    if (lds > (size_t)LDS_MAX) return fail(EEGNET_EINVAL, "eegnet_x_stats: dims need %zu B of LDS", lds);
+    const dim3 grid((unsigned)std::min<int64_t>(n, (int64_t)device_cus() * WGPC));
+    hipStream_t s = (hipStream_t)stream;
+    if (g.K1 == 32) hipLaunchKernelGGL(k_xstats<32>, grid, dim3(NTB), lds, s, g, (long long)n, x, out);
+    else hipLaunchKernelGGL(k_xstats<64>, grid, dim3(NTB), lds, s, g, (long long)n, x, out);
+    LAUNCH_CHECK("k_xstats");
+    return 0;
 }
 
 int eegnet_clamp_grads(const eegnet_dims* dims, float* grads, void* stream) {

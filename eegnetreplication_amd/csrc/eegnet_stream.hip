@@ -242,10 +242,14 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     TRACE(g, 0, TR_ENTRY);
     const int64_t* perm = nullptr;                 // fold launches: trial rows through the permutation
     long long row0 = 0;
+    // fold launches with eegnet_fold.xstat: the batch's BN1 lag sums are summed from the per-trial
+    // table (eegnet_x_stats) instead of computed from x; x is still staged for the spatial GEMM
+    const float* xst = nullptr;
     if (FOLD) {                                    // fold-indexed launch: this fold's pointers
         const eegnet_fold f = fold_rec(fc);
         prm = f.params;
         x = f.x;
+        xst = f.xstat;
         perm = f.perm; row0 = fc.row0;
         sg = (float*)((char*)f.ws + fc.off.s);
         vg = (float*)((char*)f.ws + fc.off.v);
@@ -287,11 +291,31 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
 #pragma unroll
     for (int d = 0; d < K1; ++d) G0[d] = 0.f;
     float s0 = 0.f;
-    // edge items: decode (row-index a, row-index b) once; b < 0 -> a plain sample sum
-    float eacc[NEI];
-    int ea[NEI], eb[NEI];
+    // The 22 x 256 shape (LAGM): the lag-Gram in 8-sample items (a 40-float window per 256 FMAs:
+    // 124 KB of LDS reads per 22 x 256 trial instead of 203 KB in 4-sample items), and the edge
+    // products H[a][b] = sum_c x[c][a] x[c][b] (head a, b < R) and Tl (tail) as two 16 x 16 Grams on
+    // the matrix cores -- A[m][k] = x[k][m] and B[k][n] = x[k][n] are the same lane value, so one LDS
+    // read feeds both operands (6 k-steps for C = 22: 12 MFMAs and 12 reads per trial, against 287
+    // items x 22 channels x 2 scalar LDS reads on the VALU).  Waves EW_H / EW_T run the two Grams and
+    // EW_S the head / tail sample sums, each in the second lag iteration, which only waves 0-3 fill.
+    constexpr bool LAGM = XDMA && K1 == 32 && TT == 256;    // (22 x 257: 5 VGPRs spill)
+    constexpr int EW_S = 5, EW_H = 6, EW_T = 7;
+    // xstat table row width and per-thread columns (the partial row's [G0][S0][edges] head)
+    const int NV = K1 + 1 + g.nedge;
+    constexpr int NXI = FOLD ? (K1 + 1 + KG<K1>::R * (KG<K1>::R + 1) / 2 + KG<K1>::P * (KG<K1>::P + 1) / 2 +
+                                KG<K1>::R + KG<K1>::P + NTB - 1) / NTB : 1;
+    float xacc[NXI];
 #pragma unroll
-    for (int i = 0; i < NEI; ++i) {
+    for (int k = 0; k < NXI; ++k) xacc[k] = 0.f;
+    static_assert(!LAGM || (KG<K1>::R <= 16 && KG<K1>::P <= 16), "edge Grams are one 16 x 16 tile");
+    floatx4 egram = {0.f, 0.f, 0.f, 0.f};            // wave EW_H: head Gram tile, EW_T: tail
+    float esum = 0.f;                                // wave EW_S: lane a < R head sum, R + u tail sum
+    // edge items: decode (row-index a, row-index b) once; b < 0 -> a plain sample sum
+    constexpr int NEIX = LAGM ? 1 : NEI;
+    float eacc[NEIX];
+    int ea[NEIX], eb[NEIX];
+#pragma unroll
+    for (int i = 0; i < NEIX; ++i) {
         eacc[i] = 0.f;
         int e = tid + NTB * i;
         ea[i] = -1; eb[i] = -1;
@@ -328,6 +352,51 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         const int bn = b + 1;
         pace_prio(b - b0, b1 - b0);
         spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
+        if (FOLD && xst) {
+            const float* xr = xst + (size_t)fold_row(perm, row0, b) * NV;
+#pragma unroll
+            for (int k = 0; k < NXI; ++k) {
+                const int c = tid + NTB * k;
+                if (c < NV) xacc[k] += xr[c];
+            }
+        } else if constexpr (LAGM) {
+            // lag-Gram: items (c, octet), lanes of a wave on consecutive octets of one row
+            constexpr int TO = (TT + 7) / 8;
+            for (int j = tid; j < CC * TO; j += NTB) {
+                const int c = j / TO, o = j - c * TO;
+                float w[4 * G_::NW8];
+                lds_window<G_::NW8>(Xb + c * RS + 8 * o, w);
+                float a[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) a[i] = (8 * o + i < T) ? w[G_::OFF + i] : 0.f;
+                s0 += ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+                for (int d = 0; d < K1; ++d) {
+                    float acc = G0[d];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) acc = fmaf(a[i], w[G_::OFF + i + d], acc);
+                    G0[d] = acc;
+                }
+            }
+            if (wave == EW_H || wave == EW_T) {
+                // head (x[c][a], a < R) or tail (x[c][T - P + u], u < P; u = P is the zero pad) Gram
+                const int t0 = wave == EW_H ? 0 : T - G_::P, m = lane & 15, kq = lane >> 4;
+                const float* xc = Xb + LP + t0 + m;
+#pragma unroll
+                for (int st = 0; st < KS; ++st) {
+                    const int c = 4 * st + kq;
+                    const float v = c < C ? xc[c * RS] : 0.f;
+                    egram = __builtin_amdgcn_mfma_f32_16x16x4f32(v, v, egram, 0, 0, 0);
+                }
+            } else if (wave == EW_S && lane < G_::R + G_::P) {
+                const float* xc = Xb + LP + (lane < G_::R ? lane : T - G_::P + lane - G_::R);
+                float e0 = 0.f, e1 = 0.f;
+#pragma unroll
+                for (int c = 0; c + 1 < CC; c += 2) { e0 += xc[c * RS]; e1 += xc[(c + 1) * RS]; }
+                if (CC & 1) e0 += xc[(CC - 1) * RS];
+                esum += e0 + e1;
+            }
+        } else {
         // lag-Gram: items (c, quad), lanes of a wave on consecutive quads of one row
         for (int j = tid; j < C * TQ; j += NTB) {
             const int c = j / TQ, q = j - c * TQ;
@@ -347,7 +416,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         }
         // edge outer products / sums over channels
 #pragma unroll
-        for (int i = 0; i < NEI; ++i) {
+        for (int i = 0; i < NEIX; ++i) {
             if (ea[i] >= 0) {
                 const float* xa = Xb + LP + ea[i];
                 float acc0 = 0.f, acc1 = 0.f;
@@ -366,6 +435,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
                 }
                 eacc[i] += acc0 + acc1;
             }
+        }
         }
         TRACE_PH(g, 0, 0, tph_);
         barrier_lds();                                     // Ss complete, x read for good (LDS only:
@@ -486,16 +556,147 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         }
     }
     __syncthreads();
+    if (FOLD && xst) {
+#pragma unroll
+        for (int k = 0; k < NXI; ++k) {
+            const int c = tid + NTB * k;
+            if (c < NV) pub(row + c, xacc[k]);
+        }
+    } else {
     if (tid <= K1) {
         float t = 0.f;
         for (int w = 0; w < NWB; ++w) t += red[w * (K1 + 1) + tid];
         pub(row + (tid), t);
     }
+    if constexpr (LAGM) {
+        constexpr int R_ = G_::R, P_ = G_::P, nH_ = R_ * (R_ + 1) / 2, nTl_ = P_ * (P_ + 1) / 2;
+        if (wave == EW_H || wave == EW_T) {
+            // D[m][n] of the Gram tile: lane l holds rows m = 4 (l >> 4) + r, column n = l & 15;
+            // pairs m <= n published a-major (H: a < R; Tl: u < P, after H)
+            const int n = lane & 15, E = wave == EW_H ? R_ : P_;
+            const int base = K1 + 1 + (wave == EW_H ? 0 : nH_);
 #pragma unroll
-    for (int i = 0; i < NEI; ++i)
+            for (int r = 0; r < 4; ++r) {
+                const int m = 4 * (lane >> 4) + r;
+                if (m <= n && n < E) pub(row + (base + m * E - m * (m - 1) / 2 + (n - m)), egram[r]);
+            }
+        } else if (wave == EW_S && lane < R_ + P_) {
+            pub(row + (K1 + 1 + nH_ + nTl_ + lane), esum);      // hs [R] then ts [P]
+        }
+    } else {
+#pragma unroll
+    for (int i = 0; i < NEIX; ++i)
         if (ea[i] != -2 && tid + NTB * i < g.nedge) pub(row + (K1 + 1 + tid + NTB * i), eacc[i]);
+    }
+    }
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nA, fa, dsm)) { fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa); TRACE(g, 0, TR_FIN); }
+}
+
+// ================================================================================================
+// eegnet_x_stats: the parameter-free part of pass A's BN1 statistics, per trial.  Row n of `out`:
+// [G0 K1][S0][H nH][Tl nTl][hs R][ts P] of trial n alone -- the layout of pass A's partial-row head, so
+// a fold-indexed pass A (eegnet_fold.xstat) sums a batch's rows of it in place of the lag-Gram.  One
+// trial at a time per workgroup (run once per fold set, not per step): x rows staged into LDS, the
+// 4-sample lag items and the edge items of pass A's generic path, G0 / S0 reduced over the workgroup.
+// ================================================================================================
+template <int K1>
+__global__ __launch_bounds__(NTB) void k_xstats(Geo g, long long n, const float* __restrict__ x,
+                                                float* __restrict__ out) {
+    using G_ = KG<K1>;
+    constexpr int NEI = G_::template nei<NTB>();
+    const int C = g.C, T = g.T, RS = g.RS, XP = g.XP, TQ = (T + 3) >> 2;
+    constexpr int LP = G_::LP;
+    const int NV = K1 + 1 + g.nedge;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const Xb = sm;
+    float* const red = sm + C * RS;                   // [NWB][K1 + 1]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < C * RS; i += NTB) Xb[i] = 0.f;     // pads stay zero
+    int ea[NEI], eb[NEI];
+#pragma unroll
+    for (int i = 0; i < NEI; ++i) {                   // edge items, decoded as in pass A
+        int e = tid + NTB * i;
+        ea[i] = -2; eb[i] = -1;
+        if (e < g.nH) {
+            int a = 0;
+            while (e >= g.R - a) { e -= g.R - a; ++a; }
+            ea[i] = a; eb[i] = a + e;
+        } else if ((e -= g.nH) < g.nTl) {
+            int u = 0;
+            while (e >= g.P - u) { e -= g.P - u; ++u; }
+            ea[i] = T - g.P + u; eb[i] = T - g.P + u + e;
+        } else if ((e -= g.nTl) < g.R) {
+            ea[i] = e;
+        } else if ((e -= g.R) < g.P) {
+            ea[i] = T - g.P + e;
+        }
+    }
+    for (long long b = blockIdx.x; b < n; b += gridDim.x) {
+        __syncthreads();                              // the previous trial's reads of Xb are done
+        const float* xb = x + (size_t)b * C * XP;
+        for (int i = tid; i < C * T; i += NTB) {
+            const int c = i / T, t = i - c * T;
+            Xb[c * RS + LP + t] = xb[(size_t)c * XP + t];
+        }
+        __syncthreads();
+        float G0[K1];
+#pragma unroll
+        for (int d = 0; d < K1; ++d) G0[d] = 0.f;
+        float s0 = 0.f;
+        for (int j = tid; j < C * TQ; j += NTB) {
+            const int c = j / TQ, q = j - c * TQ;
+            float w[4 * G_::NW];
+            lds_window<G_::NW>(Xb + c * RS + 4 * q, w);
+            float a[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = (4 * q + i < T) ? w[G_::OFF + i] : 0.f;
+            s0 += (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+            for (int d = 0; d < K1; ++d) {
+                float acc = G0[d];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = fmaf(a[i], w[G_::OFF + i + d], acc);
+                G0[d] = acc;
+            }
+        }
+        float* orow = out + (size_t)b * NV;
+#pragma unroll
+        for (int i = 0; i < NEI; ++i) {
+            if (ea[i] >= 0) {
+                const float* xa = Xb + LP + ea[i];
+                float acc = 0.f;
+                if (eb[i] >= 0) {
+                    const float* xb2 = Xb + LP + eb[i];
+                    for (int c = 0; c < C; ++c) acc = fmaf(xa[c * RS], xb2[c * RS], acc);
+                } else {
+                    for (int c = 0; c < C; ++c) acc += xa[c * RS];
+                }
+                orow[K1 + 1 + tid + NTB * i] = acc;
+            }
+        }
+        constexpr int NR = (K1 + 1 + 3) & ~3, NQ = NR / 4;
+        float rv[NR];
+#pragma unroll
+        for (int d = 0; d < K1; ++d) rv[d] = G0[d];
+        rv[K1] = s0;
+#pragma unroll
+        for (int i = K1 + 1; i < NR; ++i) rv[i] = 0.f;
+        wave_reduce<NR>(rv);
+        if ((lane & 15) == 0) {
+            const int r0 = (lane >> 4) * NQ;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j)
+                if (j + r0 <= K1) red[wave * (K1 + 1) + j + r0] = rv[j];
+        }
+        __syncthreads();
+        if (tid <= K1) {
+            float t = 0.f;
+            for (int w = 0; w < NWB; ++w) t += red[w * (K1 + 1) + tid];
+            orow[tid] = t;
+        }
+    }
 }
 
 // ================================================================================================

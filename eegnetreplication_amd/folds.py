@@ -44,10 +44,13 @@ class FoldBatch:
     modes, so replays draw fresh masks each step and graph and eager runs are bit-identical."""
 
     def __init__(self, models: list[EEGNet], seeds: list[int], lr=1e-3, betas=(0.9, 0.999),
-                 eps=1e-7, graphs=False, fused=None):
+                 eps=1e-7, graphs=False, fused=None, xstats=True):
         """``fused``: advance all folds with ONE launch per pass (eegnet_train_step_folds, the fold
         index in the grid) instead of one stream per fold.  ``None`` picks it whenever it applies:
-        same model shape for every fold, F1*D <= 16, and (per epoch) the same number of trials."""
+        same model shape for every fold, F1*D <= 16, and (per epoch) the same number of trials.
+        ``xstats``: fused launches read each batch's parameter-free BN1 statistics from a per-trial
+        table of every fold's X (ops.x_stats, computed once per X and refreshed when X changes in
+        place) instead of recomputing the lag-Gram from x every step."""
         if len(models) != len(seeds) or not models:
             raise ValueError("need one seed per model and at least one model")
         dev = models[0].flat_parameters().device
@@ -65,6 +68,7 @@ class FoldBatch:
         if fused and not same:
             raise ValueError("fused fold launches need the same EEGNet shape (F1*D <= 16) for every fold")
         self.fused = same if fused is None else bool(fused)
+        self.xstats = bool(xstats)
         self._fz = None                     # fused-launch state: buffers, fold tables, graph
 
     def __len__(self):
@@ -144,14 +148,16 @@ class FoldBatch:
         shape = self.models[0].shape
         xp = shape.x_pitch()
         st["x_pitch"] = 0 if xp == shape.T else xp
-        st["xpad"] = {}
+        st["xsrc"] = {}
 
         def xrows(X):
-            if ops.x_pitch_of(X) == st["x_pitch"]:
-                return X
-            if id(X) not in st["xpad"]:
-                st["xpad"][id(X)] = [X, ops.pad_x_rows(X, xp), X._version]
-            return st["xpad"][id(X)][1]
+            """(the rows the kernels read, the per-trial BN1 table or None) of X, made once per X"""
+            ent = st["xsrc"].get(id(X))
+            if ent is None:
+                rows = X if ops.x_pitch_of(X) == st["x_pitch"] else ops.pad_x_rows(X, xp)
+                stat = ops.x_stats(shape, rows) if self.xstats else None
+                ent = st["xsrc"][id(X)] = {"X": X, "rows": rows, "stat": stat, "ver": X._version}
+            return ent["rows"], ent["stat"]
         for j, i in enumerate(range(0, n, batch_size)):
             B = min(batch_size, n - i)
             st["steps"].append((i, j, B))
@@ -161,8 +167,10 @@ class FoldBatch:
                     a = self.adam[k]
                     # x / labels stay unshuffled: the kernels read batch row r as row perm[r]
                     X, y = data[k]
+                    rows, stat = xrows(X)
                     ents.append(dict(params=m.flat_parameters(), bn_buffers=m.flat_bn_buffers(),
-                                     num_batches_tracked=m.flat_num_batches_tracked(), x=xrows(X), labels=y,
+                                     num_batches_tracked=m.flat_num_batches_tracked(), x=rows, xstat=stat,
+                                     labels=y,
                                      perm=st["perm"][k], grads=a.grads, adam_state=a.state, step=a.step,
                                      losses=st["losses"][k], ws=self._workspace(k, B), seed=self.seeds[k]))
                 st["tables"][B] = ops.fold_table(ents, dev)
@@ -176,15 +184,20 @@ class FoldBatch:
             ops.train_step_folds(shape, B, st["tables"][B], K, row0=i, slot=j, offset=0, lr=self.lr,
                                  betas=self.betas, eps=self.eps, x_pitch=st["x_pitch"])
 
-    @staticmethod
-    def _refresh_padded(st):
-        """Re-copy every padded X whose source changed in place since it was padded."""
-        for ent in st["xpad"].values():
-            X, xpad, ver = ent
-            if X._version != ver:
+    def _refresh_padded(self, st):
+        """Every X that changed in place since its padded copy / BN1 table were made: re-copy and
+        recompute them in their own storage (the fold tables and the captured graph keep pointing
+        there)."""
+        shape = self.models[0].shape
+        for ent in st["xsrc"].values():
+            X = ent["X"]
+            if X._version != ent["ver"]:
                 with torch.no_grad():
-                    xpad.copy_(X)
-                ent[2] = X._version
+                    if ent["rows"] is not X:
+                        ent["rows"].copy_(X)
+                    if ent["stat"] is not None:
+                        ops.x_stats(shape, ent["rows"], out=ent["stat"])
+                ent["ver"] = X._version
 
     def _epoch_fused(self, data, batch_size, generators):
         n = data[0][0].shape[0]

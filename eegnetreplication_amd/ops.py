@@ -244,6 +244,28 @@ def stage_sums(shape: Shape, B: int, ws: torch.Tensor, p: float | None = None) -
     return out
 
 
+def x_stats(shape: Shape, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """eegnet_x_stats: the per-trial, parameter-free BN1 statistics of x [N, C, T] (contiguous or a
+    pad_x_rows view) as a [N, width] float32 device tensor -- the lag sums of each trial's zero-padded
+    rows over the channels, its window-0 sample sum and the 'same' padding's edge products / sums.
+    A fold whose training set is fixed reads a batch's rows of it instead of recomputing them."""
+    require_device(x, "x")
+    lib = _lib.load()
+    N = x.shape[0]
+    d = shape.dims(1, None, x_pitch_of(x))
+    width = int(lib.eegnet_x_stats_width(ctypes.byref(d)))
+    if width <= 0:
+        _lib.check(width, "eegnet_x_stats_width")
+    if out is None:
+        out = torch.empty((N, width), dtype=torch.float32, device=x.device)
+    elif tuple(out.shape) != (N, width) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous float32 [{N}, {width}] tensor")
+    if N:
+        _lib.check(lib.eegnet_x_stats(ctypes.byref(d), ctypes.c_int64(N), _ptr(x), _ptr(out), _stream()),
+                   "eegnet_x_stats")
+    return out
+
+
 def fold_table(entries, device) -> torch.Tensor:
     """Device array of ``eegnet_fold`` entries (a uint8 tensor holding the packed structs).
     ``entries``: dicts with the eegnet_fold fields as tensors (or None) and ``seed`` as an int."""

@@ -166,6 +166,8 @@ typedef struct eegnet_fold {
     void* ws;                       /* workspace of eegnet_workspace_bytes(dims), zeroed once     */
     const int64_t* perm;            /* epoch permutation: batch row r is x / labels row perm[r]   */
                                     /* (NULL: row r itself, i.e. x already shuffled)              */
+    const float* xstat;             /* NULL, or eegnet_x_stats(x) of this fold's x: its rows' BN1  */
+                                    /* lag sums, read instead of recomputed every epoch           */
     uint64_t seed;                  /* dropout key seed: key = mix(seed, offset + *step)          */
 } eegnet_fold;
 
@@ -181,6 +183,18 @@ typedef struct eegnet_fold {
 int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fold* folds, int64_t row0,
                             int64_t slot, uint64_t offset, float lr, float beta1, float beta2, float eps,
                             void* stream);
+
+/* Per-trial BatchNorm-1 statistics of x that do not depend on the parameters: for each of the n
+ * trials x[i] ([C][T] rows at dims->x_pitch), the lag sums of its zero-padded rows summed over the
+ * channels G0[d] (d < K1), the window-0 sample sum, and the head / tail products and sums of the
+ * 'same' padding's edges -- eegnet_x_stats_width(dims) floats per trial, written to out[n][width].
+ * BN1's batch statistics (model.py:32) are w1-quadratic forms of their sums over the batch
+ * (DESIGN.md section 3), so a fold whose training set is fixed for all epochs (train.py:87-106,
+ * 225-246) computes them once and its fold-indexed steps read the batch's rows through eegnet_fold.
+ * xstat instead of recomputing the lag-Gram (180 K of pass A's 423 K MAC per 22 x 256 trial).  The
+ * narrow path (F1*D <= 16) only; dims->B is ignored. */
+int eegnet_x_stats_width(const eegnet_dims* dims);
+int eegnet_x_stats(const eegnet_dims* dims, int64_t n, const float* x, float* out, void* stream);
 
 /* Optional per-kernel device timing for benchmarks: `on` is a bitmask of kernel ids (bit i = the
  * i-th name eegnet_profile_collect reports: k_pass_a, k_pass_b, k_pass_c, k_pass_d, k_pass_e,

@@ -142,3 +142,31 @@ def test_x_pitch_entry_point_and_validation():
     assert ok(_lib.dims(64, 32, 257, x_pitch=260)) != 0          # a runtime-shape kernel
     assert ok(_lib.dims(64, 22, 256, x_pitch=256)) == 0
     assert ok(_lib.dims(64, 22, 256, x_pitch=260)) != 0          # 22 x 256: pitch compiled in as T
+
+
+def test_fold_mirror_matches_header():
+    """The eegnet_fold mirror (_lib.Fold) and INTEGRATION.md's snippet list the header's fields in
+    order (a field added to the struct -- xstat -- shifts every later one)."""
+    from eegnetreplication_amd import _lib
+    txt = open(os.path.join(ROOT, "include", "eegnet_abi.h")).read()
+    body = re.search(r"typedef struct eegnet_fold \{(.*?)\} eegnet_fold;", txt, re.S).group(1)
+    fields = re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(\w+);", body, re.M)
+    assert fields == [n for n, _ in _lib.Fold._fields_]
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    snippet = re.search(r"class Fold\(ctypes\.Structure\):(.*?)\nassert", doc, re.S).group(1)
+    assert re.findall(r'"(\w+)"', snippet) == fields
+
+
+def test_x_stats_width_matches_pass_a_row_head():
+    """eegnet_x_stats_width = K1 + 1 + the edge items (head pairs, tail pairs, head and tail sums):
+    pass A's partial-row head a fold launch with xstat replaces."""
+    import ctypes
+    from eegnetreplication_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libeegnet_hip.so not built")
+    lib = _lib.load()
+    for K1 in (32, 64):
+        P, R = (K1 - 1) // 2, K1 - 1 - (K1 - 1) // 2
+        want = K1 + 1 + R * (R + 1) // 2 + P * (P + 1) // 2 + R + P
+        assert lib.eegnet_x_stats_width(ctypes.byref(_lib.dims(64, 22, 257, K1=K1))) == want
+    assert lib.eegnet_x_stats_width(ctypes.byref(_lib.dims(64, 64, 512, F1=16, D=4))) < 0    # narrow path only

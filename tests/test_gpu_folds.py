@@ -299,3 +299,65 @@ def test_in_place_x_update_is_seen_by_the_padded_fold_launch():
     for k in range(2):
         for a, b in zip(runs[0][k], runs[1][k]):
             assert torch.equal(a, b), f"fold {k}: the in-place update of X was not seen"
+
+
+def _x_stats_numpy(x, K1=32):
+    """float64 restatement of eegnet_x_stats for trials x [N, C, T]: [G0 K1][S0][H][Tl][hs R][ts P]
+    (G0[d] = sum_c sum_{t<T} X[t] X[t+d] with X[t] = x[t - P] zero outside [0, T))."""
+    N, Cc, Tt = x.shape
+    P, R = (K1 - 1) // 2, K1 - 1 - (K1 - 1) // 2
+    xp = np.zeros((N, Cc, Tt + P + K1), dtype=np.float64)
+    xp[:, :, P:P + Tt] = x
+    G0 = np.stack([(xp[:, :, :Tt] * xp[:, :, d:d + Tt]).sum(axis=(1, 2)) for d in range(K1)], axis=1)
+    S0 = xp[:, :, :Tt].sum(axis=(1, 2))[:, None]
+    H = [(x[:, :, a] * x[:, :, b]).sum(axis=1) for a in range(R) for b in range(a, R)]
+    Tl = [(x[:, :, Tt - P + u] * x[:, :, Tt - P + v]).sum(axis=1) for u in range(P) for v in range(u, P)]
+    hs = [x[:, :, a].sum(axis=1) for a in range(R)]
+    ts = [x[:, :, Tt - P + u].sum(axis=1) for u in range(P)]
+    return np.concatenate([G0, S0, np.stack(H + Tl + hs + ts, axis=1)], axis=1)
+
+
+@pytest.mark.parametrize("Tt,pitched", [(256, False), (257, False), (257, True)])
+def test_x_stats_match_numpy(Tt, pitched):
+    """eegnet_x_stats (per-trial BN1 lag sums, window sums, edge products) against a float64 numpy
+    restatement, for the recordings' 22 x 257 (contiguous and at the 260-float pitch) and 22 x 256."""
+    from eegnetreplication_amd import EEGNet, ops
+    dev = _dev()
+    rng = np.random.default_rng(19)
+    x = rng.standard_normal((37, C, Tt)).astype(np.float32)
+    X = torch.from_numpy(x).to(dev)
+    shape = EEGNet(C, Tt).shape
+    if pitched:
+        X = ops.pad_x_rows(X, shape.x_pitch())
+    got = ops.x_stats(shape, X).cpu().numpy()
+    ref = _x_stats_numpy(x.astype(np.float64))
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+
+
+def test_fold_launch_with_x_stats_matches_recomputed():
+    """Fold launches reading the per-trial BN1 table (FoldBatch(xstats=True), the default) against
+    the same folds recomputing the lag-Gram from x every step (xstats=False): the same training to
+    fp32 rounding (the batch sums are formed in another order), over three epochs at p = 0; and the
+    table follows an in-place change of X."""
+    from golden_util import assert_params_close
+    from eegnetreplication_amd import FoldBatch
+    dev = _dev()
+    data = [_data(150, 700 + k, dev) for k in range(3)]
+    runs = []
+    for xs in (True, False):
+        models = _models(3, 0.0, dev)
+        fb = FoldBatch(models, [1, 2, 3], graphs=True, fused=True, xstats=xs)
+        gens = [torch.Generator().manual_seed(s) for s in (1, 2, 3)]
+        Xs = [(X.clone(), y) for X, y in data]
+        for e in range(3):
+            if e == 2:
+                Xs[1][0].mul_(0.5)                   # in place: the table must be recomputed
+            fb.epoch(Xs, 64, gens)
+        torch.cuda.synchronize()
+        runs.append(fb)
+    for k in range(3):
+        a, b = runs[0].models[k], runs[1].models[k]
+        assert_params_close({n: p.detach().cpu().numpy() for n, p in a.named_parameters()},
+                            {n: p.detach().cpu().numpy() for n, p in b.named_parameters()}, steps=9,
+                            rtol=1e-4, atol_frac=1e-4, prefix=f"fold {k} xstats vs recomputed ")

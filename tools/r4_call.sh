@@ -28,7 +28,7 @@ print('cpu', (d.get('cpu_baseline') or {}).get('value'), [(l['cores'], l['value'
 fi
 if [ -n "$AB" ]; then
   for i in 1 2; do
-    for tree in abtrees/r3g abtrees/r3end .; do
+    for tree in ${TREES:-abtrees/r3g abtrees/r3end .}; do
       ( cd $tree && timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-infer --no-folds --no-cfg5 --no-cfg4 --steps 50 ) > gpurun_out/${TAG}_ab_$(basename $tree)_$i.log 2>&1 || { echo AB_FAILED $tree; tail -20 gpurun_out/${TAG}_ab_$(basename $tree)_$i.log; exit 1; }
       tail -1 gpurun_out/${TAG}_ab_$(basename $tree)_$i.log | TREE=$tree python3 -c "
 import json,sys,os; d=json.loads(sys.stdin.read())
