@@ -408,6 +408,20 @@ struct Stage {
     }
 };
 
+// A wave-uniform load through the constant address space: the scalar unit (s_load, counted by
+// lgkmcnt), so a prologue's weight / coefficient loads are not queued behind -- vmcnt being in order --
+// the first trial's LDS-DMA and plane loads issued before them.  Only for data no workgroup of the
+// running kernel writes before every workgroup has passed its prologue (parameters, the previous
+// launches' coefficients: the scalar cache is invalidated at every kernel start).
+template <typename T>
+__device__ __forceinline__ T ldc(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(4))) T*)p;
+#else
+    return *p;
+#endif
+}
+
 // a wave-uniform zero the compiler cannot see through: added to a weight-row offset it pins that
 // row's scalar loads next to their use (otherwise every row of every table is hoisted into SGPRs and
 // spilled)

@@ -455,7 +455,7 @@ __device__ __forceinline__ void adam_slice_range(const Geo& g, int part, int npa
 __device__ __forceinline__ void adam_scalars_publish(const Geo& g, const FinArgs& fa) {
     if (blockIdx.x != 0 || threadIdx.x != 0 || !adam_early(g, fa)) return;
     float step_size, bc2s;
-    adam_scalars(fa, *fa.step + 1, step_size, bc2s);
+    adam_scalars(fa, ldc(fa.step) + 1, step_size, bc2s);
     pub(fa.coef + CF_ADAM * CSTR, step_size);
     pub(fa.coef + CF_ADAM * CSTR + 1, bc2s);
 }
@@ -465,7 +465,7 @@ __device__ __forceinline__ void adam_scalars_publish(const Geo& g, const FinArgs
 // pass E calls this in its prologue (its finalize is a later launch), the narrow one passes the value
 // it read in its prologue.
 __device__ __forceinline__ int adam_step0(const Geo& g, const FinArgs& fa) {
-    return adam_early(g, fa) ? __builtin_amdgcn_readfirstlane(*fa.step) : 0;
+    return adam_early(g, fa) ? ldc(fa.step) : 0;        // scalar load: not behind the prologue's DMAs
 }
 __device__ void adam_slice(const Geo& g, const FinArgs& fa, int part, int nparts, int step0) {
     if (!adam_early(g, fa)) return;

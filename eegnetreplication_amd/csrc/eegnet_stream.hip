@@ -206,9 +206,10 @@ __device__ __forceinline__ void half_taps(const float (&tap)[NTS][K1], int hr, f
 }
 
 // Temporal taps of this wave's rows: one shared set for the specialised EEGNet-8,2 shapes (the
-// rows 2w, 2w+1 of a wave are group w when D = 2), one set per row otherwise.  The taps are
-// wave-uniform: readfirstlane keeps them in SGPRs even when prm comes from a fold record (an ordinary
-// load, whose result the compiler would otherwise hold per lane: K1 VGPRs per tap set).
+// rows 2w, 2w+1 of a wave are group w when D = 2), one set per row otherwise.  Wave-uniform scalar
+// loads (ldc): the taps land in SGPRs even when prm comes from a fold record, and the prologue does
+// not wait on them behind the first trial's DMA (no pass writes w1 before every prologue is done: fin5's
+// Adam runs after the last workgroup has published).
 template <int K1, int NTS>
 __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict__ prm, int D, int F2, int wave,
                                           float (&tap)[NTS][K1]) {
@@ -218,7 +219,7 @@ __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict_
         const int gg = (o < F2 ? o : 0) / D;
 #pragma unroll
         for (int k = 0; k < K1; ++k)
-            tap[r][k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(prm[g.o_w1 + gg * K1 + k])));
+            tap[r][k] = ldc(prm + (g.o_w1 + gg * K1 + k));
     }
 }
 
@@ -1047,12 +1048,21 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     if constexpr (XDMA) zero_pads(sm, 2 * F2 + C, RS, LP, T, tid);   // the data windows are DMA'd / written
     load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
     TRACE_PS(g, 2);
-    if (tid < 8 * F2) {
-        const int o = tid >> 3, f = tid & 7;
-        const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
-                         : f == 2 ? prm + g.o_g2 : f == 3 ? prm + g.o_b2 : f == 4 ? coef + CF_AO * CSTR
-                         : f == 5 ? coef + CF_BO * CSTR : coef + CF_CO * CSTR;
-        CT[tid] = src[o];
+    {   // the BN2 forward / backward constants of this wave's rows [o][8], by scalar loads (ldc: not
+        // queued behind the DMAs above; coef is the earlier finalizes', g2 / b2 change only in fin5)
+        float cv = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8 * RPW; ++k) {
+            const int o = RPW * wave + (k >> 3), f = k & 7;
+            if (o < F2 && f < 7) {
+                const float* src = f == 0 ? coef + CF_AL2 * CSTR : f == 1 ? coef + CF_BE2 * CSTR
+                                 : f == 2 ? prm + g.o_g2 : f == 3 ? prm + g.o_b2 : f == 4 ? coef + CF_AO * CSTR
+                                 : f == 5 ? coef + CF_BO * CSTR : coef + CF_CO * CSTR;
+                const float v = ldc(src + o);
+                cv = lane == k ? v : cv;
+            }
+        }
+        if (lane < 8 * RPW && RPW * wave + (lane >> 3) < F2) CT[8 * RPW * wave + lane] = cv;
     }
     adam_scalars_publish(g, fa);
     const int step0 = adam_step0(g, fa);           // before the reduction ticket (adam_slice)

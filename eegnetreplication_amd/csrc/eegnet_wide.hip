@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         CT[tid] = src[orr];
     }
     const int NO = (T + 7) >> 3;
-    constexpr int MOW = 2;                                 // octets per lane: T <= 1024
+    constexpr int MOW = SPEC ? 1 : 2;                      // octets per lane: T <= 1024 (cfg5: 512, one)
     float sdyl = 0.f, sdyvl = 0.f;
     // this wave's row of the dW1 lag correlation on the matrix cores, as in k_pass_e:
     // Cq[u][w] = sum_a dy[16a+u] s'[16a+w] accumulated over the trials, Q[k] = sum_u Cq[u][u+k]
@@ -1218,29 +1218,46 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                 }
             }
         }
-        if (bn < b1) stage_rows(bn);                       // the next trial's s / dp2 rows of this wave
-        barrier_lds();                                     // e rows complete
-        // Xm[o][c] += sum_t e[o][t] x[c][t]: A = e rows (LDS), B = x (global), float4 k-permuted
-        if (gemm_on) {
-            const int c = ct * 16 + li;
-            const bool bon = c < C;
-            const float* arow = Dys + li * RS + LP + 4 * lk;
-            const float* xr = x + ((size_t)b * C + (bon ? c : 0)) * T + 4 * lk;
-            for (int kg = kg0; kg < kg1; ++kg) {
-                const int t0 = 16 * kg + 4 * lk;
-                floatx4 b4;
+        // Xm[o][c] += sum_t e[o][t] x[c][t]: A = e rows (LDS), B = x (global / L2), float4 k-permuted.
+        // This wave's x operand goes out XPF k-groups at a time, the first batch BEFORE the next rows'
+        // DMA and the barrier: its latency overlaps the other waves' FIR^T (loaded one k-group per
+        // iteration inside the GEMM, every load waited for its own round trip).
+        constexpr int XPF = 4;
+        const int cx = ct * 16 + li;
+        const bool bon = cx < C;
+        const float* xr = x + ((size_t)b * C + (bon ? cx : 0)) * T + 4 * lk;
+        floatx4 xpf[XPF];
+        auto xload = [&](int kgs) {
+#pragma unroll
+            for (int i = 0; i < XPF; ++i) {
+                const int kg = min(kgs + i, kg1 - 1), t0 = 16 * kg + 4 * lk;
                 if ((T & 3) == 0 && t0 + 3 < T) {
-                    b4 = *reinterpret_cast<const floatx4*>(xr + 16 * kg);
+                    xpf[i] = *reinterpret_cast<const floatx4*>(xr + 16 * kg);
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) b4[e] = (t0 + e < T) ? xr[16 * kg + e] : 0.f;
+                    for (int e = 0; e < 4; ++e) xpf[i][e] = (t0 + e < T) ? xr[16 * kg + e] : 0.f;
                 }
-                if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                const floatx4 a4 = lds_ld4(arow + 16 * kg);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
+            }
+        };
+        if (gemm_on && kg0 < kg1) xload(kg0);
+        if (bn < b1) stage_rows(bn);                       // the next trial's s / dp2 rows of this wave
+        barrier_lds();                                     // e rows complete
+        if (gemm_on) {
+            const float* arow = Dys + li * RS + LP + 4 * lk;
+            for (int kgs = kg0; kgs < kg1; kgs += XPF) {   // (one batch at cfg5: 8 k-groups per wave)
+#pragma unroll
+                for (int i = 0; i < XPF; ++i) {
+                    const int kg = kgs + i;
+                    if (kg < kg1) {
+                        const floatx4 a4 = lds_ld4(arow + 16 * kg);
+                        const floatx4 b4 = bon ? xpf[i] : (floatx4){0.f, 0.f, 0.f, 0.f};
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
+                    }
+                }
+                if (kgs + XPF < kg1) xload(kgs + XPF);
             }
         }
         barrier_vm<0>();                                   // e rows consumed; next rows landed

@@ -54,6 +54,11 @@ def _pink_noise(rng, shape, T):
     return np.fft.irfft(np.fft.rfft(white, axis=-1) * scale, n=T, axis=-1)
 
 
+# population / subject parameters of the synthetic sessions: each subject draws its mu and beta
+# frequencies, its class-effect strength and its spatial-mixing jitter from these ranges
+SYNTH_PARAMS = dict(mu=(9.0, 11.5), beta=(19.0, 24.0), strength=(0.25, 0.6), mix=0.15)
+
+
 def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C=N_CHANNELS,
                       T=N_SAMPLES) -> BCICI2ADataset:
     """Seeded SMR-like session: classes 0..3 = left hand / right hand / feet /
@@ -70,10 +75,11 @@ def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C
     y = rng.permutation(np.concatenate([y, rng.integers(0, 4, n - y.size)]))
     t = np.arange(T) / SFREQ
     X = _pink_noise(rng, (n, C, T), T) * 2.0
-    mu_f = srng.uniform(9.0, 11.5)
-    beta_f = srng.uniform(19.0, 24.0)
-    strength = srng.uniform(0.25, 0.6)      # tuned so the stock reference reaches ~30-80 %
-    mix = np.eye(C) + 0.15 * srng.standard_normal((C, C))
+    sp = SYNTH_PARAMS
+    mu_f = srng.uniform(*sp["mu"])
+    beta_f = srng.uniform(*sp["beta"])
+    strength = srng.uniform(*sp["strength"])      # tuned so the stock reference reaches ~30-80 %
+    mix = np.eye(C) + sp["mix"] * srng.standard_normal((C, C))
     for i in range(n):
         ph = rng.uniform(0, 2 * np.pi, 2)
         rhythm = np.sin(2 * np.pi * mu_f * t + ph[0]) + 0.5 * np.sin(2 * np.pi * beta_f * t + ph[1])

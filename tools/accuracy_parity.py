@@ -155,7 +155,97 @@ def run_reference(spec, epochs, dev, common):
     return 100.0 * float((out.argmax(1).cpu() == torch.as_tensor(te[1])).float().mean())
 
 
-def _worker(wid, jobs, protocol, cs_folds, epochs, common, q):
+def _keep_t(n: int, key: torch.Tensor, pthr: int, dev) -> torch.Tensor:
+    """_keep with the 32-bit key a device tensor (graph-capturable: the key is read, not baked in)."""
+    h = torch.arange(n, dtype=torch.int64, device=dev)
+    h = (h * 0x9E3779B1 + key) & M32
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & M32
+    h = h ^ (h >> 16)
+    return (h >> 8) >= pthr
+
+
+def run_reference_graphed(spec, epochs, dev, common):
+    """run_reference with each epoch's training steps captured once as a CUDA graph and replayed
+    (the reference is launch-bound at batch 64: ~80 small kernels per step).  The same layer stack,
+    loss, clamps and batch order; Adam with capturable=True (its bias corrections as device tensors:
+    the same formula, rounding-level differences); the common-mask keys of every step precomputed and
+    read in the graph through a device step counter; the epoch's permutation copied into the graph's
+    static buffer before each replay.  The first epoch runs eagerly (Adam's state is created lazily)."""
+    from eegnetreplication_amd.dataset import epoch_permutation
+    from eegnetreplication_amd.model import EEGNet
+    from oracle import torch_ref as tr
+    import torch.nn.functional as F
+    X, y, tr_ids, va_ids, te, p, seed = spec
+    torch.manual_seed(seed)
+    init = EEGNet(C=X.shape[1], T=X.shape[2], p=p)
+    ref = tr.TorchRefEEGNet({k: v.numpy() for k, v in init.state_dict().items()}, p=p, device=dev)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3, eps=1e-7, capturable=True)
+    gen = torch.Generator().manual_seed(seed)
+    Xt = torch.as_tensor(X[tr_ids], dtype=torch.float32, device=dev)
+    yt = torch.as_tensor(y[tr_ids], dtype=torch.int64, device=dev)
+    n = len(yt)
+    F2, T = init.F1 * init.D, X.shape[2]
+    T1, T2 = T // 4, (T // 4) // 8
+    nsteps = -(-n // 64)
+    keys = None
+    pthr = int(min(16777216.0, max(0.0, float(np.float32(p)) * 16777216.0)))
+    if common and p > 0:
+        kk = []
+        for st in range(epochs * nsteps):
+            key = mix_key(seed, st)
+            kk.append([key & M32, ((key >> 32) ^ 0x5BD1E995) & M32])
+        keys = torch.tensor(kk, dtype=torch.int64, device=dev)
+    step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    perm_buf = torch.zeros(n, dtype=torch.int64, device=dev)
+    for prm in ref.parameters():
+        prm.grad = torch.zeros_like(prm)
+
+    def epoch_body():
+        for i in range(0, n, 64):
+            idx = perm_buf[i:i + 64]
+            B = idx.shape[0]
+            masks = None
+            if keys is not None:
+                kr = keys.index_select(0, step_t)[0]
+                masks = (_keep_t(B * F2 * T1, kr[0], pthr, dev).view(B, F2, T1),
+                         _keep_t(B * F2 * T2, kr[1], pthr, dev).view(B, F2, T2))
+            logits = ref(Xt.index_select(0, idx), masks)
+            loss = F.cross_entropy(logits, yt.index_select(0, idx))
+            opt.zero_grad(set_to_none=False)
+            loss.backward()
+            opt.step()
+            step_t.add_(1)
+
+    ref.training = True
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream())
+    graph = None
+    with torch.cuda.stream(s):
+        for e in range(epochs):
+            perm_buf.copy_(epoch_permutation(n, gen).to(dev))
+            if e == 0:
+                epoch_body()                         # eager: Adam's state, cuDNN/MIOpen plans
+                continue
+            if graph is None:
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+                saved = step_t.clone()
+                with torch.cuda.graph(graph, stream=s):
+                    epoch_body()
+                step_t.copy_(saved)                  # (capture recorded, did not run)
+            graph.replay()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    ref.training = False                     # train() leaves the model in eval mode (model.py:151)
+    with torch.no_grad():
+        out = ref(torch.as_tensor(te[0], dtype=torch.float32, device=dev))
+    return 100.0 * float((out.argmax(1).cpu() == torch.as_tensor(te[1])).float().mean())
+
+
+def _worker(wid, jobs, protocol, cs_folds, epochs, common, q, graphed=True):
     """Reference units (seed, unit index) -> (seed, unit, accuracy); specs regenerated here."""
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
@@ -164,7 +254,7 @@ def _worker(wid, jobs, protocol, cs_folds, epochs, common, q):
         if seed not in cache:
             cache = {seed: specs_for(protocol, seed, cs_folds)}
         t0 = time.perf_counter()
-        acc = run_reference(cache[seed][u], epochs, dev, common)
+        acc = (run_reference_graphed if graphed else run_reference)(cache[seed][u], epochs, dev, common)
         q.put((seed, u, acc, time.perf_counter() - t0))
 
 
@@ -194,6 +284,8 @@ def main():
                     default=[10 * s + r for s in range(9) for r in range(2)],
                     help="0-based cross-subject fold indices (default: repeats 1-2 of every subject)")
     ap.add_argument("--workers", type=int, default=8, help="reference worker processes on the GPU")
+    ap.add_argument("--ref-eager", action="store_true",
+                    help="train the reference units step by step (no CUDA graph; the original driver)")
     ap.add_argument("--out", type=str, default="")
     args = ap.parse_args()
     from eegnetreplication_amd.train import _run_units
@@ -210,7 +302,7 @@ def main():
     q = ctx.Queue()
     nw = max(1, min(args.workers, len(jobs)))
     procs = [ctx.Process(target=_worker, args=(w, jobs[w::nw], args.protocol, args.cs_folds, args.epochs,
-                                                common, q)) for w in range(nw)]
+                                                common, q, not args.ref_eager)) for w in range(nw)]
     t_start = time.perf_counter()
     for p in procs:
         p.start()
