@@ -106,16 +106,16 @@ __device__ __forceinline__ void stage_aw_chunk(const Geo& g, const float* __rest
 }
 
 // x rows [c0, c0 + nc) of one trial into padded LDS rows (data window [LP, LP + T)): LDS-DMA of
-// 256-sample pieces when T is a multiple of 256 (no registers; drains at the next barrier), else a
-// plain copy
+// 256-sample pieces when T is a multiple of 256 (no registers; from inline asm, as eegnet_stream.hip's
+// dma16, so the compiler does not make the next LDS read of ANY address wait for it: the caller's
+// barrier drains it), else a plain copy
 __device__ __forceinline__ void stage_slice(const float* __restrict__ xs, int nc, int T, int RS, int LP, float* Xg,
                                             int tid, int wave, int lane) {
     if ((T & 255) == 0) {
         const int np = T >> 8;
         for (int i = wave; i < nc * np; i += NWW) {
             const int c = i / np, p = i - c * np;
-            __builtin_amdgcn_global_load_lds((gvoid_t*)(xs + (size_t)c * T + 256 * p + 4 * lane),
-                                             (lvoid_t*)(Xg + c * RS + LP + 256 * p), 16, 0, 0);
+            dma16(xs + (size_t)c * T + 256 * p + 4 * lane, Xg + c * RS + LP + 256 * p);
         }
     } else {
         for (int i = tid; i < nc * T; i += NTW) {
@@ -197,8 +197,11 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     }
     __syncthreads();                                   // zero fill done before the first slice lands
     if (b0 < b1 && nc > 0) stage_slice(x + ((size_t)b0 * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
-    __syncthreads();
+    barrier_vm<0>();                                   // the first slice landed (asm DMA: explicit vmcnt)
     drain_prologue_loads();
+    // the cfg5 geometry: every wave owns a row, whose s and v stores are SV_ST wave-instructions (2 v
+    // octet halves + T / 256 s pieces); the closing barrier lets exactly those stay in flight
+    constexpr int SV_ST = 2 + 512 / 256;
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
         spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
@@ -233,7 +236,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 eacc[i] += acc;
             }
         }
-        __syncthreads();                                   // s rows complete, slice read for good
+        barrier_lds();                                     // s rows complete, slice read for good (LDS
+                                                           // only: no stores of this trial are out yet)
         if (bn < b1 && nc > 0) stage_slice(x + ((size_t)bn * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
         if (row_on) {
             const float* row = Ss + wave * RS;
@@ -259,7 +263,10 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 for (int t = lane; t < T; t += 64) srow[t] = row[LP + t];
             }
         }
-        __syncthreads();                                   // next slice staged, s rows free
+        // next slice staged (its DMA precedes this trial's s / v stores: vmcnt is in order), s rows
+        // free; at cfg5 the SV_ST stores stay in flight into the next trial
+        if constexpr (SPEC) barrier_vm<SV_ST>();
+        else barrier_vm<0>();
     }
 
     // ---- workgroup reduction -> one partial row (other chunks' Sv / Sv2 entries are zero) ----
