@@ -93,10 +93,14 @@ class DataParallelTrainer:
         self.lr, self.betas, self.eps = lr, betas, eps
         self.group = group
         self.broadcast_buffers = broadcast_buffers
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # collectives run whenever a process group exists -- at world 1 too, where each is an
+        # identity (x 1/1, rank 0's own buffers) and the step stays bit-identical to FusedTrainer:
+        # that is how a one-GPU box exercises the RCCL path (tests/test_gpu_distributed.py)
+        self.dist = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.dist else 1
+        self.rank = dist.get_rank(group) if self.dist else 0
         flat = model.flat_parameters()
-        if self.world > 1:   # identical start on every rank: parameters, BN buffers and counters
+        if self.dist:        # identical start on every rank: parameters, BN buffers and counters
             self.broadcast_state()
         self._init_state(flat)
         self._ws = {}
@@ -144,7 +148,7 @@ class DataParallelTrainer:
     def reduce(self, grads):
         """ONE all-reduce (SUM) of [grads | loss | rank 0's BN buffers], then x 1/world on the
         gradient and the loss (CE is a batch mean) and rank 0's buffers into every rank's BN."""
-        if self.world == 1:
+        if not self.dist:
             return grads
         n = grads.numel()
         bn = self.model.flat_bn_buffers()
@@ -177,7 +181,7 @@ class DataParallelTrainer:
         ranks' local batches, all-reduced every step (a short last batch on one rank -- a sampler with
         drop_last=False -- must not mis-normalise every rank's statistics and gradients).  One small
         collective and a host read per step, in the sync_bn path only."""
-        if self.world == 1:
+        if not self.dist:
             return B
         t = torch.tensor([B], dtype=torch.float64, device=self.model.flat_parameters().device)
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
@@ -202,7 +206,7 @@ class DataParallelTrainer:
 
     def reduce_sums(self, sums):
         """ONE all-reduce (SUM) of a pass's fp64 sums."""
-        if self.world > 1:
+        if self.dist:
             dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)
         return sums
 

@@ -299,3 +299,53 @@ def test_sync_bn_world2_equals_single_device_on_the_whole_batch():
     for got, ref, what in ((res[0][4], m.flat_bn_buffers(), "bn"), (res[0][5], fu.adam.state, "adam")):
         ref = ref.detach().cpu().numpy()
         np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6 * float(np.abs(ref).max()), err_msg=what)
+
+
+def _rccl_worker(port, q):
+    """World 1 over the nccl (= RCCL) backend in a fresh process: DataParallelTrainer runs its real
+    collectives (broadcast of the start point, the per-step all-reduce of [grads | loss | buffers],
+    the sync-BN batch and per-pass sums) through RCCL on the device."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from eegnetreplication_amd import FusedTrainer
+    from eegnetreplication_amd.distributed import DataParallelTrainer
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        out = {"backend": str(dist.get_backend())}
+        g = Golden("G1")
+        x = torch.from_numpy(g.x).to(dev)
+        y = torch.from_numpy(g.y).to(dev)
+        for sync in (False, True):
+            a, b = _model_from(g, dev), _model_from(g, dev)
+            dp, fu = DataParallelTrainer(a, sync_bn=sync), FusedTrainer(b)
+            same_loss = all(float(dp.step(x, y)) == float(fu.step(x, y)) for _ in range(3))
+            torch.cuda.synchronize()
+            out[sync] = (dp.dist, same_loss, torch.equal(a.flat_parameters(), b.flat_parameters()),
+                         torch.equal(a.flat_bn_buffers(), b.flat_bn_buffers()),
+                         torch.equal(dp.adam.state, fu.adam.state))
+        dist.destroy_process_group()
+        q.put((out, None))
+    except Exception as e:                 # report instead of hanging the parent
+        q.put((None, repr(e)))
+        raise
+
+
+def test_dp_trainer_over_rccl_world1():
+    """The RCCL (backend "nccl") branch on the one-GPU box: at world 1 every collective is an identity,
+    so DataParallelTrainer -- plain and sync_bn -- stays bit-identical to FusedTrainer over 3 steps
+    while each of its broadcasts and all-reduces runs through RCCL."""
+    import torch.multiprocessing as mp
+    _dev()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    out, err = q.get(timeout=150)
+    p.join(timeout=60)
+    assert err is None, err
+    assert p.exitcode == 0
+    assert out["backend"] == "nccl"
+    for sync in (False, True):
+        assert out[sync] == (True, True, True, True, True), (sync, out[sync])
