@@ -96,6 +96,26 @@ __device__ __forceinline__ void spatial_chunk(const float* __restrict__ xb, cons
     }
 }
 
+// The cfg5 geometry (C = 64, T = 512: NT16 = 32 tiles, two per wave, all 16 k-steps in range): the
+// B operands of tile m of this wave for trial xb (k_wpass_a loads the first tile's a trial ahead), and
+// the tile's GEMM into the s rows
+constexpr int SPT = 2;                 // spatial tiles per wave at cfg5
+__device__ __forceinline__ void spatial_load5(const float* __restrict__ xb, float (&bv)[KSW], int m, int wave, int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < KSW; ++s) bv[s] = xb[(size_t)(4 * s + lk) * 512 + 16 * (wave + NWW * m) + li];
+}
+__device__ __forceinline__ void spatial_mfma5(const float (&bv)[KSW], const float* awl, float* Ss, int RS, int LP, int m,
+                                              int wave, int lane) {
+    const int li = lane & 15, lk = lane >> 4;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KSW; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(awl[64 * s + lane], bv[s], acc, 0, 0, 0);
+    const int t = 16 * (wave + NWW * m) + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Ss[(4 * lk + r) * RS + LP + t] = acc[r];
+}
+
 // the ws fragment table of chunk rows [o0, o0 + 16) into LDS (KSW * 64 floats)
 __device__ __forceinline__ void stage_aw_chunk(const Geo& g, const float* __restrict__ prm, int o0, float* awl,
                                                int tid, int nth) {
@@ -195,8 +215,14 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
             ea[i] = -2;
         }
     }
+    // cfg5: the B operands of this wave's first spatial tile of the next trial (the second tile's
+    // are loaded at the top of the trial and land behind the first tile's MFMAs; holding both across
+    // the FIR spilled 10 VGPRs)
+    float bv5[SPEC ? KSW : 1], bw5[SPEC ? KSW : 1];
     __syncthreads();                                   // zero fill done before the first slice lands
     if (b0 < b1 && nc > 0) stage_slice(x + ((size_t)b0 * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
+    if constexpr (SPEC)
+        if (b0 < b1) spatial_load5(x + (size_t)b0 * C * T, bv5, 0, wave, lane);
     barrier_vm<0>();                                   // the first slice landed (asm DMA: explicit vmcnt)
     drain_prologue_loads();
     // the cfg5 geometry: every wave owns a row, whose s and v stores are SV_ST wave-instructions (2 v
@@ -204,7 +230,16 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     constexpr int SV_ST = 2 + 512 / 256;
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
-        spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
+        if constexpr (SPEC) {
+            spatial_load5(x + (size_t)b * C * T, bw5, 1, wave, lane);
+            spatial_mfma5(bv5, awl, Ss, RS, LP, 0, wave, lane);
+            // the next trial's first-tile operands: in flight over the second tile, the lag-Gram and
+            // the FIR, drained (vmcnt is in order) by this trial's closing barrier
+            if (bn < b1) spatial_load5(x + (size_t)bn * C * T, bv5, 0, wave, lane);
+            spatial_mfma5(bw5, awl, Ss, RS, LP, 1, wave, lane);
+        } else {
+            spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
+        }
         for (int c = wave; c < nc; c += NWW) {
             const float* xr = Xg + c * RS + G_::OFF + li;        // xp[i - P] = row[OFF + i]
             for (int ks = 0; ks < KQ; ++ks) {
