@@ -251,37 +251,79 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     const double* Sv2 = Sv + F2;
     // lag-Gram of the padded rows: G[k][k+d] = G0[d] + sum_{j<k} Ed[d][j], with
     // Ed[d][j] = sum_c X[T+j]X[T+j+d] - X[j]X[j+d] = Tl[j][j+d] (j+d < P) - H[j-P][j-P+d] (j >= P).
-    // Lag d is one lane's serial prefix over k (its loads do not depend on the chain: unrolled, they
-    // issue ahead of the adds).
-    if (tid < K1) {
-        const int d = tid;
-        const double base = G0[d];
-        double e = 0.0;
-#pragma unroll 8
-        for (int k = 0; k < K1; ++k) {
-            if (k + d < K1) {
-                const double v = base + e;
+    // Lag d is a group of 8 lanes, lane q owning positions k = 4q .. 4q + 3 (K1 <= 32) or 8q .. 8q + 7
+    // (K1 = 64): each lane sums its own Ed terms, the group's exclusive prefix over q takes three
+    // shuffles, then each lane writes its positions.  (A serial 32-step prefix per lag, one lane each,
+    // took 5.5 µs of the 9.4 µs finalize: every step waited an LDS round trip.)
+    const int KPL = K1 <= 32 ? 4 : 8;                 // positions per lane
+    if (tid < 8 * K1) {
+        const int d = tid >> 3, q = tid & 7, k0 = KPL * q;
+        double ed[8], seg = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = k0 + i;
+            double v = 0.0;
+            if (i < KPL && k < K1 - 1 - d) {
+                if (k + d < g.P) v += Tl[k * g.P - k * (k - 1) / 2 + d];
+                if (k >= g.P) {
+                    const int a = k - g.P;
+                    v -= H[a * g.R - a * (a - 1) / 2 + d];
+                }
+            }
+            ed[i] = v;
+            seg += v;
+        }
+        // exclusive prefix of the segment sums over the 8 lanes of lag d
+        double inc = seg;
+#pragma unroll
+        for (int sh = 1; sh < 8; sh <<= 1) {
+            const double u = __shfl_up(inc, sh, 8);
+            if (q >= sh) inc += u;
+        }
+        double v = G0[d] + (inc - seg);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = k0 + i;
+            if (i < KPL && k + d < K1) {
                 Gm[k * GS + k + d] = v;
                 Gm[(k + d) * GS + k] = v;
-                double ed = 0.0;
-                if (k < K1 - 1 - d) {
-                    if (k + d < g.P) ed += Tl[k * g.P - k * (k - 1) / 2 + d];
-                    if (k >= g.P) {
-                        const int a = k - g.P;
-                        ed -= H[a * g.R - a * (a - 1) / 2 + d];
-                    }
-                }
-                e += ed;
             }
-        }
-    } else if (tid == 64) {           // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j])
-        double e = 0.0;
-        for (int k = 0; k < K1; ++k) {
-            S1[k] = S0 + e;
-            e += (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
+            v += ed[i];
         }
     }
+    // window sums S1[k] = S0 + sum_{j<k} (X[T+j] - X[j]): the same 8-lane segmented prefix, by the 8
+    // lanes after the lag groups (K1 = 64 at 512 threads: lanes 0-7, after a barrier)
+    auto window_sums = [&](int q) {
+        const int k0 = KPL * q;
+        double es[8], seg = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int k = k0 + i;
+            double v = 0.0;
+            if (i < KPL && k < K1) v = (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
+            es[i] = v;
+            seg += v;
+        }
+        double inc = seg;
+#pragma unroll
+        for (int sh = 1; sh < 8; sh <<= 1) {
+            const double u = __shfl_up(inc, sh, 8);
+            if (q >= sh) inc += u;
+        }
+        double v = S0 + (inc - seg);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i < KPL && k0 + i < K1) S1[k0 + i] = v;
+            v += es[i];
+        }
+    };
+    const bool s1_now = 8 * K1 + 8 <= nth;
+    if (s1_now && tid >= 8 * K1 && tid < 8 * K1 + 8) window_sums(tid - 8 * K1);
     __syncthreads();
+    if (!s1_now) {
+        if (tid < 8) window_sums(tid);
+        __syncthreads();
+    }
     TRACE_FS(g, fa.tpass, 4);
     // G w1 per (filter, tap): row k of the symmetric G, four partial chains
     for (int p = tid; p < F1 * K1; p += nth) {
