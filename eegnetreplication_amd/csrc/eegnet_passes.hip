@@ -307,6 +307,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     if (!(mode & PC_BWD)) return;
     // ---- workgroup reduction: every wave writes a full partial row, then the waves are summed ----
     __syncthreads();
+    TRACE_PS(g, 8);
     float* red = sm;                         // [nw][nC]
     float* rw = red + wave * g.nC;
 #pragma unroll
@@ -317,6 +318,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
             if (i < NF) rw[n * NF + i] = wacc[n][u];
         }
     wave_reduce<2 * F2MAX>(sdz);
+    TRACE_PS(g, 9);
     if ((lane & 15) == 0) {
         const int r0 = (lane >> 4) * (F2MAX / 2);
 #pragma unroll
@@ -332,8 +334,10 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
         rw[NCLS * NF + NCLS + 2 * F2] = lossacc;
     }
     __syncthreads();
+    TRACE_PS(g, 10);
     float* row = part + (size_t)blockIdx.x * g.nC;
     for (int c = tid; c < g.nC; c += blockDim.x) pub(row + c, wave_rows_sum<NTH / 64>(red, nw, g.nC, c));
+    TRACE_PS(g, 11);
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
 }

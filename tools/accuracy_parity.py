@@ -321,6 +321,11 @@ def main():
         if i % 8 == 7 or i == len(jobs) - 1:
             print(f"  reference {i + 1}/{len(jobs)} units ({time.perf_counter() - t_start:.0f} s, "
                   f"last {secs:.1f} s)", flush=True)
+            if args.out:                      # progress record: what a run cut off by its time limit had
+                with open(args.out + ".partial", "w") as fo:
+                    json.dump({"hip": {str(k): v for k, v in hip.items()},
+                               "ref": [[sd, uu, a] for (sd, uu), a in ref.items()],
+                               "elapsed_s": round(time.perf_counter() - t_start, 1)}, fo)
     for p in procs:
         p.join(timeout=120)
     pairs = []

@@ -89,6 +89,12 @@ def main():
             if ks:
                 print("    prologue stamps (µs after entry, mean over workgroups):",
                       " ".join(f"{k}:{np.mean(ps[:, k]-ent)/100:.2f}" for k in ks), f"pro:{np.mean(pro-ent)/100:.2f}")
+        if p == 2:
+            ps = a[7, :grids[p], 8:12]
+            if (ps > 0).any():
+                print("    tail stamps (µs after the loop, mean over workgroups): "
+                      "waves joined %.2f | sdz reduced %.2f | rows in LDS %.2f | row published %.2f"
+                      % tuple(np.mean(ps[:, k] - loop) / 100 for k in range(4)))
         ph = st[:, 8:16].mean(axis=0) / ntr
         if ph.any():
             print("    in-loop phases (shader cycles per trial, wave 0):", " ".join(f"{v:.0f}" for v in ph))
