@@ -213,8 +213,10 @@ __host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1, int ng) {
 // matrix-vector products G w1 as (filter, tap) lanes with four partial chains, and the filters' sums
 // over taps from LDS -- no shuffle scans.  G w1 and S1 go to fa.stats for fin5 (dW1 needs exactly those,
 // the same parameters being in force through pass E).
+template <int K1>
 __device__ void fin1(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
-    const int K1 = g.K1, F1 = g.F1, F2 = g.F2, C = g.C, nth = blockDim.x;
+    const int F1 = g.F1, F2 = g.F2, C = g.C, nth = blockDim.x;
+    constexpr int P = (K1 - 1) / 2, R = K1 - 1 - P, NH = R * (R + 1) / 2, NTL = P * (P + 1) / 2;
     const int GS = K1 + 1;            // padded row stride of G and Ed (conflict-free column walks)
     double* Gm = scr;                 // K1 * GS
     double* S1 = Gm + K1 * GS;        // K1
@@ -244,32 +246,34 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     const double* G0 = sums;
     const double S0 = sums[K1];
     const double* H = sums + K1 + 1;                 // head pairs (a <= b < R), a-major
-    const double* Tl = H + g.nH;                     // tail pairs (u <= v < P), u-major
-    const double* hs = Tl + g.nTl;                   // head sample sums [R]
-    const double* ts = hs + g.R;                     // tail sample sums [P]
-    const double* Sv = ts + g.P;
+    const double* Tl = H + NH;                       // tail pairs (u <= v < P), u-major
+    const double* hs = Tl + NTL;                     // head sample sums [R]
+    const double* ts = hs + R;                       // tail sample sums [P]
+    const double* Sv = ts + P;
     const double* Sv2 = Sv + F2;
     // lag-Gram of the padded rows: G[k][k+d] = G0[d] + sum_{j<k} Ed[d][j], with
     // Ed[d][j] = sum_c X[T+j]X[T+j+d] - X[j]X[j+d] = Tl[j][j+d] (j+d < P) - H[j-P][j-P+d] (j >= P).
     // Lag d is a group of 8 lanes, lane q owning positions k = 4q .. 4q + 3 (K1 <= 32) or 8q .. 8q + 7
     // (K1 = 64): each lane sums its own Ed terms, the group's exclusive prefix over q takes three
     // shuffles, then each lane writes its positions.  (A serial 32-step prefix per lag, one lane each,
-    // took 5.5 µs of the 9.4 µs finalize: every step waited an LDS round trip.)
-    const int KPL = K1 <= 32 ? 4 : 8;                 // positions per lane
+    // took 5.5 µs of the 9.4 µs finalize: every step waited an LDS round trip.)  Every load is
+    // unconditional at a clamped index (a guarded load is a branch and a wait each) and selected after.
+    constexpr int KPL = K1 / 8;                       // positions per lane
     if (tid < 8 * K1) {
         const int d = tid >> 3, q = tid & 7, k0 = KPL * q;
-        double ed[8], seg = 0.0;
+        double tv[KPL], hv[KPL];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < KPL; ++i) {
+            const int k = k0 + i, a = k - P;
+            tv[i] = Tl[min(max(k * P - k * (k - 1) / 2 + d, 0), NTL - 1)];
+            hv[i] = H[min(max(a * R - a * (a - 1) / 2 + d, 0), NH - 1)];
+        }
+        double ed[KPL], seg = 0.0;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
             const int k = k0 + i;
-            double v = 0.0;
-            if (i < KPL && k < K1 - 1 - d) {
-                if (k + d < g.P) v += Tl[k * g.P - k * (k - 1) / 2 + d];
-                if (k >= g.P) {
-                    const int a = k - g.P;
-                    v -= H[a * g.R - a * (a - 1) / 2 + d];
-                }
-            }
+            const bool on = k < K1 - 1 - d;
+            const double v = (on && k + d < P ? tv[i] : 0.0) - (on && k >= P ? hv[i] : 0.0);
             ed[i] = v;
             seg += v;
         }
@@ -282,9 +286,9 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
         }
         double v = G0[d] + (inc - seg);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < KPL; ++i) {
             const int k = k0 + i;
-            if (i < KPL && k + d < K1) {
+            if (k + d < K1) {
                 Gm[k * GS + k + d] = v;
                 Gm[(k + d) * GS + k] = v;
             }
@@ -295,12 +299,12 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     // lanes after the lag groups (K1 = 64 at 512 threads: lanes 0-7, after a barrier)
     auto window_sums = [&](int q) {
         const int k0 = KPL * q;
-        double es[8], seg = 0.0;
+        double es[KPL], seg = 0.0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < KPL; ++i) {
             const int k = k0 + i;
-            double v = 0.0;
-            if (i < KPL && k < K1) v = (k < g.P ? ts[k] : 0.0) - (k >= g.P ? hs[k - g.P] : 0.0);
+            const double tsv = ts[min(k, P - 1)], hsv = hs[min(max(k - P, 0), R - 1)];
+            const double v = (k < P ? tsv : 0.0) - (k >= P ? hsv : 0.0);
             es[i] = v;
             seg += v;
         }
@@ -312,8 +316,8 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
         }
         double v = S0 + (inc - seg);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (i < KPL && k0 + i < K1) S1[k0 + i] = v;
+        for (int i = 0; i < KPL; ++i) {
+            S1[k0 + i] = v;
             v += es[i];
         }
     };
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(512) void k_fin(Geo g, const float* prm, FinArgs fa
     __syncthreads();
     double* scr = dfin + tail_s_doubles(ncols);
     switch (pass) {
-        case 0: fin1(g, prm, S, scr, fa); break;
+        case 0: if (g.K1 == 32) fin1<32>(g, prm, S, scr, fa); else fin1<64>(g, prm, S, scr, fa); break;
         case 1: fin2(g, S, fa); break;
         case 2: fin3(g, prm, S, fa); break;
         case 3: fin4(g, prm, S, fa); break;

@@ -591,7 +591,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     }
     }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nA, fa, dsm)) { fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa); TRACE(g, 0, TR_FIN); }
+    if (grid_reduce(g, part, g.nA, fa, dsm)) { fin1<K1>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa); TRACE(g, 0, TR_FIN); }
 }
 
 // ================================================================================================

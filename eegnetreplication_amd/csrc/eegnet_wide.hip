@@ -345,7 +345,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
         pub(row + (K1 + 1 + g.nedge + q), v);
     }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nA, fa, dsm)) fin1(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa);
+    if (grid_reduce(g, part, g.nA, fa, dsm)) fin1<K1>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa);
 }
 
 // ================================================================================================
