@@ -55,8 +55,13 @@ def _pink_noise(rng, shape, T):
 
 
 # population / subject parameters of the synthetic sessions: each subject draws its mu and beta
-# frequencies, its class-effect strength and its spatial-mixing jitter from these ranges
-SYNTH_PARAMS = dict(mu=(9.0, 11.5), beta=(19.0, 24.0), strength=(0.25, 0.6), mix=0.15)
+# frequencies, its class-effect strength and its spatial-mixing jitter from these ranges.  Round 4
+# (tools/synth_cs_sweep.py preset "v9"; profiles/r4d_sweep.log): a shared class signature -- the same
+# C3 / C4 / Cz topography with narrow mu / beta bands and a small per-subject mixing jitter -- so the
+# cross-subject protocol learns (68.6 % at 500 epochs, per test subject 38-97 %) and the within-subject
+# one is not saturated (86.1 %).  Round 3's ranges (mu 9-11.5 Hz, beta 19-24 Hz, strength 0.25-0.6,
+# mix 0.15) left cross-subject at 31 %, near the 25 % chance level.
+SYNTH_PARAMS = dict(mu=(9.5, 10.5), beta=(20.0, 22.0), strength=(0.35, 0.65), mix=0.06)
 
 
 def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C=N_CHANNELS,
@@ -65,8 +70,8 @@ def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C
     tongue.  Hand imagery desynchronises the mu (8-12 Hz) and beta (18-26 Hz) rhythm over the
     contralateral sensorimotor cortex (C4 for left, C3 for right), feet over Cz, tongue weakly
     everywhere; each subject gets its own strength and spatial mixing, on top of 1/f noise.  The
-    effect sizes put the reference model's per-subject test accuracy in the 30-80 % range of the
-    reference's own BCI IV-2a reports, so accuracy comparisons are not saturated.
+    effect sizes (SYNTH_PARAMS) put per-subject test accuracy in the 40-100 % range (cross-subject
+    mean 69 %, within-subject 86 %), so both protocols learn and neither comparison is saturated.
     Trials are standardised per channel like the reference's exponential moving standardisation."""
     sess = 0 if mode == "Train" else 1
     rng = np.random.default_rng(1000 * subject + 17 * sess + 3)
@@ -78,7 +83,7 @@ def synthetic_session(subject: int, mode: str = "Train", n=TRIALS_PER_SESSION, C
     sp = SYNTH_PARAMS
     mu_f = srng.uniform(*sp["mu"])
     beta_f = srng.uniform(*sp["beta"])
-    strength = srng.uniform(*sp["strength"])      # tuned so the stock reference reaches ~30-80 %
+    strength = srng.uniform(*sp["strength"])
     mix = np.eye(C) + sp["mix"] * srng.standard_normal((C, C))
     for i in range(n):
         ph = rng.uniform(0, 2 * np.pi, 2)
