@@ -150,12 +150,12 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->gridS = std::min(g->B, device_cus() * WGPC * grid_mult());     // streaming passes A, B, E
     const int rows1 = g->C * g->RS;                   // x rows (one buffer)
     const int nf4 = rup(g->NF, 4);
-    g->ldsA = rows1 + g->F2 * g->RS + NWB * (g->K1 + 1);
+    const bool spec = g->C == 22 && (g->T == 256 || g->T == 257) && g->F1 == 8 && g->D == 2 && g->K1 == 32;   // EEG_DISPATCH
+    g->ldsA = (spec ? 2 : 1) * rows1 + g->F2 * g->RS + NWB * (g->K1 + 1);   // compile-time shapes: two x buffers
     g->ldsB = 3 * g->F2 * g->RS2 + F2MAX * (K2 + F2MAX);
     // passes C / D: one trial stream per wave, each with its own block-2 rows (row_stride_b2)
     g->RSW = row_stride_b2(g->T1);
     const int pwC = nf4, pwD = 3 * g->F2 * g->RSW + nf4;
-    const bool spec = g->C == 22 && (g->T == 256 || g->T == 257) && g->F1 == 8 && g->D == 2 && g->K1 == 32;   // EEG_DISPATCH
     g->nwC = std::max(1, std::min(spec ? NWAVE : NTHS / 64, (LDS_MAX / 4) / pwC));
     g->nwD = std::max(1, std::min(NTHS / 64, (LDS_MAX / 4) / pwD));
     g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);

@@ -265,20 +265,23 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     constexpr int NEI = G_::template nei<NTB>();
     const int D = FF ? 2 : g.D;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* const Xb = sm;              // one x buffer: the next trial lands after its last reader
-    float* Ss = sm + C * RS;
+    constexpr bool XDMA = TT != 0;                    // compile-time shapes: x / s rows by LDS-DMA
+    // x buffers: compile-time shapes double-buffer x (trial b + 1 goes out by DMA at the top of trial
+    // b, a whole trial ahead of its use); the others stage through registers into one buffer
+    constexpr int NXB = XDMA ? 2 : 1;
+    float* Xb = sm;
+    float* Ss = sm + NXB * C * RS;
     float* red = Ss + F2 * RS;                        // NWB * (K1 + 1)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int b0, b1;
     trial_range(g, b0, b1);
 
-    constexpr bool XDMA = TT != 0;                    // compile-time shapes: x / s rows by LDS-DMA
     // compile-time shapes: the first trial's x goes out by LDS-DMA before anything else; the pad fill,
     // the weight loads and the edge decode below overlap it, and one barrier waits for all of it
     if constexpr (XDMA) {
         if (b0 < b1) x_dma_asm(x + fold_row(perm, row0, b0) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
-        zero_pads(sm, C + F2, RS, LP, T, tid);
+        zero_pads(sm, NXB * C + F2, RS, LP, T, tid);
     } else {
         zero_fill<false>(sm, (C + F2) * RS, C, RS, LP, T, tid);
     }
@@ -352,6 +355,15 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
         pace_prio(b - b0, b1 - b0);
+        if constexpr (XDMA) {
+            // this trial's buffer; the next trial's x into the other one, whose last reader (the
+            // previous trial) finished before the previous closing barrier.  It lands by this trial's
+            // closing barrier, a whole trial later (one buffer gave it only the FIR: ~1,500 shader
+            // cycles per trial waited for it, profiles/r4d_timeline.txt phase 4).
+            Xb = sm + ((b - b0) & 1) * C * RS;
+            if (bn < b1) x_dma_asm(x + fold_row(perm, row0, bn) * (C * XP), C, T, XP, RS, LP,
+                                   sm + ((bn - b0) & 1) * C * RS, wave, lane);
+        }
         spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
         if (FOLD && xst) {
             const float* xr = xst + (size_t)fold_row(perm, row0, b) * NV;
@@ -441,10 +453,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         TRACE_PH(g, 0, 0, tph_);
         barrier_lds();                                     // Ss complete, x read for good (LDS only:
                                                            // the previous trial's v stores stay in flight)
-        if (bn < b1) {                                     // next x: lands by the closing barrier
-            if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, bn) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
-            else x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * XP), C, T, pf, tid);   // live over the FIR only
-        }
+        if constexpr (!XDMA)
+            if (bn < b1) x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * XP), C, T, pf, tid);   // live over the FIR only
         TRACE_PH(g, 0, 1, tph_);
         // s rows -> the s plane [B][F2][T] (pass E's lag-correlation operand)
         s_rows_store<NTB>(Ss, sg + (size_t)b * F2 * s_pitch(T), F2, T, RS, LP, tid);
