@@ -315,9 +315,21 @@ def main():
         hip[seed] = [r["test_acc"] for r in out]
         print(f"seed {seed}: HIP {np.mean(hip[seed]):.2f}% ({time.perf_counter() - t0:.1f} s)", flush=True)
     ref = {}
+    import queue as _queue
     for i in range(len(jobs)):
-        seed, u, acc, secs = q.get(timeout=3000)
+        waited = 0
+        while True:                           # a heartbeat line a minute: a silent run reads as hung
+            try:
+                seed, u, acc, secs = q.get(timeout=60)
+                break
+            except _queue.Empty:
+                waited += 60
+                print(f"  waiting for reference unit {i + 1}/{len(jobs)} "
+                      f"({time.perf_counter() - t_start:.0f} s)", flush=True)
+                if waited >= 3000 or not any(p.is_alive() for p in procs):
+                    raise RuntimeError("reference workers stopped without a result")
         ref[(seed, u)] = acc
+        print(f"  reference unit seed {seed} #{u}: {acc:.2f}% in {secs:.1f} s", flush=True)
         if i % 8 == 7 or i == len(jobs) - 1:
             print(f"  reference {i + 1}/{len(jobs)} units ({time.perf_counter() - t_start:.0f} s, "
                   f"last {secs:.1f} s)", flush=True)

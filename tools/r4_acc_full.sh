@@ -11,4 +11,4 @@ FARGS=""
 timeout -k 10 ${LIMIT:-1120} python -u tools/accuracy_parity.py --protocol ${PROTO:-cs} --epochs ${EPOCHS:-500} \
   --seeds ${SEEDS:-0} --workers ${WORKERS:-15} --dropout ${DROP:-common} $FARGS --out gpurun_out/$TAG.json \
   > gpurun_out/$TAG.log 2>&1 || { echo ACC_FAILED; tail -20 gpurun_out/$TAG.log; exit 1; }
-grep -v "^  reference" gpurun_out/$TAG.log | tail -6
+grep -v -E "^  (reference|waiting)" gpurun_out/$TAG.log | tail -6
