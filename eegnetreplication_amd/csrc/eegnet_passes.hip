@@ -420,12 +420,21 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
     TRACE(g, 3, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
-    for (int b = blockIdx.x * nw + wave; b < g.B; b += gridDim.x * nw) {
-        float dlv[NCLS];
+    // a trial's pass-B rows (d2, q, r) and dlogits go out together -- one global round trip, not three
+    // -- and the next trial's are loaded into the same registers as soon as this trial has consumed
+    // them (after the BN3 backward), so they land during the dW3 / dq / dw2 / dd2 phases
+    float dlv[NCLS];
+    float d[F2MAX][MQ], q[F2MAX][MQ], r[F2MAX][MQ];
+    auto load_trial = [&](int bb) {
 #pragma unroll
-        for (int n = 0; n < NCLS; ++n) dlv[n] = dl[(size_t)b * NCLS + n];
-        float d[F2MAX][MQ];
-        load_rows<MQ>(d2g, b, F2, T1, lane, d);
+        for (int n = 0; n < NCLS; ++n) dlv[n] = dl[(size_t)bb * NCLS + n];
+        load_rows<MQ>(d2g, bb, F2, T1, lane, d);
+        load_rows<MQ>(q3g, bb, F2, T1, lane, q);
+        load_rows<MQ>(r3g, bb, F2, T1, lane, r);
+    };
+    const int bstep = gridDim.x * nw;
+    if (blockIdx.x * nw + wave < g.B) load_trial(blockIdx.x * nw + wave);
+    for (int b = blockIdx.x * nw + wave; b < g.B; b += bstep) {
         // d2 rows -> P0 (read back by the dw2 correlation)
 #pragma unroll
         for (int o = 0; o < F2MAX; ++o)
@@ -444,8 +453,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
             if (i < NF) Hs[i] = dd * keep_mul(g, mask3, dk1, (unsigned)(b * NF + i));
         }
         TRACE_PH(g, 3, 0, tph_);
-        float q[F2MAX][MQ];                     // block-2 depthwise output: pass B's q plane
-        load_rows<MQ>(q3g, b, F2, T1, lane, q);
+        // block-2 depthwise output (pass B's q plane) -> P1
 #pragma unroll
         for (int o = 0; o < F2MAX; ++o)
 #pragma unroll
@@ -460,11 +468,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
         float dr[F2MAX][MQ];
         {
             float xh[F2MAX][MQ];
-            {
-                float r[F2MAX][MQ];                 // pointwise output: pass B's r plane
-                load_rows<MQ>(r3g, b, F2, T1, lane, r);
-                bn3_rows<MQ>(coef, F2, r, xh);
-            }
+            bn3_rows<MQ>(coef, F2, r, xh);          // r: pass B's pointwise output
 #pragma unroll
             for (int j = 0; j < F2MAX; ++j) {
                 if (j < F2) {
@@ -487,10 +491,12 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
         }
         wave_lds_fence();
         TRACE_PH(g, 3, 2, tph_);
-        // E1 / E2 of pass B for the BN2-backward sums at the end (issued here, consumed last)
+        // E1 / E2 of pass B for the BN2-backward sums at the end (issued here, consumed last), then
+        // the next trial's rows (younger: the E1 / E2 wait does not wait for them)
         float e1v[F2MAX][MQ], e2v[F2MAX][MQ];
         load_rows<MQ>(E1g, b, F2, T1, lane, e1v);
         load_rows<MQ>(E2g, b, F2, T1, lane, e2v);
+        if (b + bstep < g.B) load_trial(b + bstep);
         // dW3[j][i] += sum_t dr[j][t] q[i][t] on the matrix cores (float4 k-permuted operands)
         {
             const bool on = li < F2;
