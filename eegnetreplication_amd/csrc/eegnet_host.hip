@@ -221,7 +221,8 @@ static int make_geo_wide(Geo* g, bool launch) {
     const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables
     b2_lds(g, NWB2);
     g->gridB2 = g->grid;
-    g->ldsWE = std::max(std::max(2 * 16 * g->RS + rup(16 * g->T1, 4) + 8 * 16 + awl, NWW * 256 + 32 + NWW * 256 * ((15 + g->K1 - 1) / 16 + 1)),
+    // s rows, dy / e rows x 2 (alternate trials), dp2 rows, coefficient table
+    g->ldsWE = std::max(std::max(3 * 16 * g->RS + rup(16 * g->T1, 4) + 8 * 16 + awl, NWW * 256 + 32 + NWW * 256 * ((15 + g->K1 - 1) / 16 + 1)),
                         tailw(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->o_g2)));
     g->ldsWI = 16 * g->RS + b2 + nf4 + 4 * g->F2P + g->NOC * awl;
     (void)nf4;

@@ -1084,10 +1084,10 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
 // come from pass A's planes; every wave stages and reads only its own s / dy / dp2 rows until the
 // dws GEMM, which reads all e rows of the chunk and x (global memory, L2).
 // Partial row [Q F2*K1][Xm F2*C][Sdy F2][Sdyv F2] (other chunks' entries zero).
-// LDS: s rows [16][RS] | dy rows, then (in place) e [16][RS] | dp2 rows [16][T1] | coefficient table
+// LDS: s rows [16][RS] | dy rows, then (in place) e [16][RS], two buffers (alternate trials) | dp2 rows [16][T1] | coefficient table
 // [16][8]; after the loop: dws tiles [NWW][256], row sums, lag-correlation tiles [NWW][16][16 NWT]
 // Per trial and wave: v (loaded a trial ahead) -> dy2 | next dp2 row (DMA) | lag correlation |
-// FIR^T -> e over the dy row | next s row (DMA) | barrier | dws GEMM | barrier
+// FIR^T -> e over the dy row | next s row (DMA) | barrier | dws GEMM | own DMAs landed (no barrier)
 // ================================================================================================
 template <int K1, bool SPEC = false>
 __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, const float* coef,
@@ -1103,13 +1103,15 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
     wide_unit(g, j, b0, b1, rr);
     const int o0 = 16 * j, nrows = min(16, F2 - o0);
     float* Ss = sm;
-    float* Dys = Ss + 16 * RS;
-    float* DP = Dys + 16 * RS;
+    // dy / e rows, two buffers (alternate trials): the next trial's dy2 phase writes the other one
+    // while slower waves still read this trial's e rows in the dws GEMM, so one barrier per trial
+    float* const Dys0 = Ss + 16 * RS;
+    float* DP = Dys0 + 2 * 16 * RS;
     float* CT = DP + ((16 * T1 + 3) & ~3);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    for (int i = tid; i < 2 * 16 * RS; i += NTW) sm[i] = 0.f;
+    for (int i = tid; i < 3 * 16 * RS; i += NTW) sm[i] = 0.f;
     const int o = o0 + wave;
     const bool row_on = wave < nrows;
     const int oo = row_on ? o : 0;
@@ -1175,6 +1177,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
+        float* const Dys = Dys0 + ((b - b0) & 1) * 16 * RS;
         float vc[MOW][8];
 #pragma unroll
         for (int m = 0; m < MOW; ++m)
@@ -1302,7 +1305,10 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                 if (kgs + XPF < kg1) xload(kgs + XPF);
             }
         }
-        barrier_vm<0>();                                   // e rows consumed; next rows landed
+        // no second barrier: the next trial writes the other dy / e buffer (this one is rewritten two
+        // trials on, after the next trial's barrier, which every wave passes only once its GEMM here
+        // is done); its s / dp2 rows are this wave's own, so the wave waits for its own DMAs only
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 
