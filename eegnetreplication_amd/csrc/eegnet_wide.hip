@@ -931,6 +931,24 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
     // dw2 item of this thread: row o2, taps 4 kq .. 4 kq + 3
     const int o2 = tid >> 2, kq = tid & 3;
     float acc2[4] = {0.f, 0.f, 0.f, 0.f};
+    // cfg5 (compile-time F2 = 64, T1 = 128, 512 threads): a trial's d2 / q / r rows are four float4
+    // per thread and plane, loaded into registers a whole trial ahead and stored to LDS at the top of
+    // the trial; the dd2 phase loads its items' E1 / E2 two items at a time (each of the four items
+    // waited one global round trip for them; all four at once, or from the top of the trial, spill)
+    constexpr bool PFD = SPEC && NT == 512;
+    constexpr int NPD = 4;                             // float4 per thread and plane at cfg5
+    floatx4 pd[PFD ? 3 : 1][PFD ? NPD : 1], pe1[PFD ? NPD : 1], pe2[PFD ? NPD : 1];
+    auto planes_load = [&](int bb) {
+        const floatx4* s0 = reinterpret_cast<const floatx4*>(d2g + (size_t)bb * F2 * T1);
+        const floatx4* s1 = reinterpret_cast<const floatx4*>(q3g + (size_t)bb * F2 * T1);
+        const floatx4* s2 = reinterpret_cast<const floatx4*>(r3g + (size_t)bb * F2 * T1);
+#pragma unroll
+        for (int j = 0; j < NPD; ++j) {
+            pd[0][j] = s0[tid + NT * j]; pd[1][j] = s1[tid + NT * j]; pd[2][j] = s2[tid + NT * j];
+        }
+    };
+    if constexpr (PFD)
+        if ((int)blockIdx.x < g.B) planes_load(blockIdx.x);
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
@@ -938,9 +956,21 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
 #pragma unroll
         for (int n = 0; n < NCLS; ++n) dlv[n] = dl[(size_t)b * NCLS + n];
         const size_t rb = (size_t)b * F2 * T1;
-        b2_stage(d2g + rb, F2, T1, RB, D2, tid, NT);
-        b2_stage(q3g + rb, F2, T1, RB, Q, tid, NT);
-        b2_stage(r3g + rb, F2, T1, RB, DR, tid, NT);      // r rows, then dr in place
+        if constexpr (PFD) {
+            constexpr int TQ1C = 128 / 4;
+#pragma unroll
+            for (int j = 0; j < NPD; ++j) {
+                const int i = tid + NT * j, o = i / TQ1C, qq = i - o * TQ1C;
+                lds_st4(D2 + o * RB + LQW + 4 * qq, pd[0][j]);
+                lds_st4(Q + o * RB + LQW + 4 * qq, pd[1][j]);
+                lds_st4(DR + o * RB + LQW + 4 * qq, pd[2][j]);
+            }
+            if (b + (int)gridDim.x < g.B) planes_load(b + gridDim.x);   // registers free again
+        } else {
+            b2_stage(d2g + rb, F2, T1, RB, D2, tid, NT);
+            b2_stage(q3g + rb, F2, T1, RB, Q, tid, NT);
+            b2_stage(r3g + rb, F2, T1, RB, DR, tid, NT);  // r rows, then dr in place
+        }
         // dh -> dropout -> dp3 (flattened) into Hd
 #pragma unroll
         for (int u = 0; u < MAXNFW; ++u) {
@@ -1023,7 +1053,7 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
             }
         }
         // dd2[t] = sum_k w2[k] dq[t + 7 - k] -> dropout -> dp2; BN2-backward sums (E1 / E2 of pass B)
-        for (int it = tid; it < nit; it += NT) {
+        auto dd2_item = [&](int it, const float* e1, const float* e2) {
             const int o = it / TQ1, qd = it - o * TQ1;
             float s1 = 0.f, s2 = 0.f;
             float w[24];
@@ -1040,12 +1070,31 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
                     const size_t gi = rb + (size_t)o * T1 + t;
                     const float dp = a * keep_mul(g, mask2, dk0, (unsigned)gi);
                     dp2g[gi] = dp;
-                    s1 = fmaf(dp * 0.25f, E1g[gi], s1);
-                    s2 = fmaf(dp * 0.25f, E2g[gi], s2);
+                    s1 = fmaf(dp * 0.25f, e1 ? e1[i] : E1g[gi], s1);
+                    s2 = fmaf(dp * 0.25f, e2 ? e2[i] : E2g[gi], s2);
                 }
             }
             IS[it] += s1;                                  // this thread's own slots
             IS[nit + it] += s2;
+        };
+        if constexpr (PFD) {
+#pragma unroll
+            for (int h = 0; h < NPD; h += 2) {         // two items' E1 / E2 per round trip
+#pragma unroll
+                for (int j = h; j < h + 2; ++j) {
+                    const int it = tid + NT * j, o = it / (128 / 4), qd = it - o * (128 / 4);
+                    pe1[j] = *reinterpret_cast<const floatx4*>(E1g + rb + o * 128 + 4 * qd);
+                    pe2[j] = *reinterpret_cast<const floatx4*>(E2g + rb + o * 128 + 4 * qd);
+                }
+#pragma unroll
+                for (int j = h; j < h + 2; ++j) {
+                    const float e1[4] = {pe1[j][0], pe1[j][1], pe1[j][2], pe1[j][3]};
+                    const float e2[4] = {pe2[j][0], pe2[j][1], pe2[j][2], pe2[j][3]};
+                    dd2_item(tid + NT * j, e1, e2);
+                }
+            }
+        } else {
+            for (int it = tid; it < nit; it += NT) dd2_item(it, nullptr, nullptr);
         }
         __syncthreads();                                   // D2, Q, DR, Hd free for the next trial
     }
