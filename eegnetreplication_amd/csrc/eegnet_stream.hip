@@ -517,7 +517,11 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         if constexpr (!XDMA)
             if (bn < b1) x_store<PF, NTB>(pf, C, T, RS, LP, Xb, tid);
         TRACE_PH(g, 0, 3, tph_);
-        if constexpr (XDMA) barrier_vm<0>();               // next x landed (asm DMA: explicit vmcnt), Ss free
+        // next x landed (asm DMA, issued at the top of the trial: explicit vmcnt), Ss free.  The
+        // trial's s-plane stores are younger than that DMA, so the barrier lets them stay in flight:
+        // s_rows_store issues F2 s_pitch(T) / 4 / NTB float4 stores per thread -- 2 at 22 x 256, 2 or
+        // 3 at 22 x 257 (vmcnt(2) waits for the DMA either way)
+        if constexpr (XDMA) barrier_vm<2>();
         else __syncthreads();                              // Xb staged, Ss free
         if constexpr (DEFER) {
             if (o < F2) {
