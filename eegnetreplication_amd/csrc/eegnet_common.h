@@ -90,7 +90,7 @@ struct Geo {
     X(o_ws, 544) X(o_g2, 4640) X(o_b2, 4704) X(o_w2, 4768) X(o_W3, 5792) X(o_g3, 9888) X(o_b3, 9952) \
     X(o_Wfc, 10016) X(o_bfc, 14112) X(nparam, 14116) X(nA, 448) X(nB, 128) X(nC, 4229) X(nD, 5248)    \
     X(nE, 6272) X(QR, 64) X(wide, 1) X(NOC, 4) X(CPC, 16) X(F2P, 64) X(RB, 144) X(splitC, 1)         \
-    X(splitD, 1) X(splitE, 1) X(ldsWA, 19120) X(ldsWB, 0) X(ldsWB2, 23872) X(ldsWC, 10528)           \
+    X(splitD, 1) X(splitE, 1) X(ldsWA, 36656) X(ldsWB, 0) X(ldsWB2, 23872) X(ldsWC, 10528)           \
     X(ldsWD, 37952) X(ldsWE, 29504) X(ldsWI, 37760)
 __host__ __device__ __forceinline__ void shape_w5(Geo& g) {
 #define EEG_SET_(f, v) g.f = v;

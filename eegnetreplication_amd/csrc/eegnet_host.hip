@@ -214,7 +214,9 @@ static int make_geo_wide(Geo* g, bool launch) {
     const int awl = KSW * 64;                               // spatial GEMM fragment table
     // after the loop pass A's Gram tiles [NWW][16][16 NWT] reuse the slice / s rows when they fit
     const int cgw = NWW * 256 * ((15 + g->K1 - 1) / 16 + 1);
-    const int baseA = (g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW + awl;
+    // the cfg5 shape (k_wpass_a's SPEC instantiation) double-buffers the slice and the s rows
+    const bool w5 = g->C == 64 && g->T == 512 && g->F1 == 16 && g->D == 4 && g->K1 == 32;
+    const int baseA = (w5 ? 2 : 1) * (g->CPC + 16) * g->RS + NWW * (g->K1 + 1) + 2 * NWW + awl;
     g->ldsWA = std::max(baseA + ((g->CPC + 16) * g->RS >= cgw ? 0 : cgw),
                         tailw(g->nA, std::max(NTH, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C))));
     g->ldsWB = 0;                                           // k_wpass_b: registers only (v plane)

@@ -167,13 +167,16 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     wide_unit(g, j, b0, b1);
     const int o0 = 16 * j;
     const int c0 = j * g.CPC, nc = max(0, min(g.CPC, C - c0));      // this workgroup's Gram slice
+    // cfg5: slice and s rows double-buffered over alternate trials (one workgroup barrier per trial,
+    // below); 147 KB of LDS
+    constexpr int NBUF = SPEC ? 2 : 1;
     float* Xg = sm;
-    float* Ss = Xg + g.CPC * RS;
-    float* red = Ss + 16 * RS;
+    float* Ss = Xg + NBUF * g.CPC * RS;
+    float* red = Ss + NBUF * 16 * RS;
     float* awl = red + NWW * (K1 + 1) + 2 * NWW;        // ws fragments [KSW][64]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < (g.CPC + 16) * RS; i += NTW) sm[i] = 0.f;
+    for (int i = tid; i < NBUF * (g.CPC + 16) * RS; i += NTW) sm[i] = 0.f;
     stage_aw_chunk(g, prm, o0, awl, tid, NTW);
     const int o = o0 + wave;
     const bool row_on = o < F2;
@@ -230,13 +233,26 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     constexpr int SV_ST = 2 + 512 / 256;
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
+        // cfg5: this trial's buffers.  Per trial: spatial GEMM -> s rows | barrier (s rows complete,
+        // this trial's slice landed) | lag-Gram + edges on the slice | next slice's DMA into the other
+        // buffer | FIR of the own row -> v, s planes.  The next trial's spatial GEMM writes the other s
+        // buffer (last read by this trial's predecessor's FIR, before this trial's barrier) and its
+        // slice DMA the other slice buffer (last read by the predecessor's lag-Gram, idem): no closing
+        // barrier.
         if constexpr (SPEC) {
+            Xg = sm + ((b - b0) & 1) * g.CPC * RS;
+            Ss = sm + 2 * g.CPC * RS + ((b - b0) & 1) * 16 * RS;
             spatial_load5(x + (size_t)b * C * T, bw5, 1, wave, lane);
             spatial_mfma5(bv5, awl, Ss, RS, LP, 0, wave, lane);
             // the next trial's first-tile operands: in flight over the second tile, the lag-Gram and
-            // the FIR, drained (vmcnt is in order) by this trial's closing barrier
+            // the FIR
             if (bn < b1) spatial_load5(x + (size_t)bn * C * T, bv5, 0, wave, lane);
             spatial_mfma5(bw5, awl, Ss, RS, LP, 1, wave, lane);
+            // s rows complete; this trial's slice (DMA'd in the previous trial, before the previous
+            // FIR's SV_ST stores and this trial's 2 x KSW operand loads) landed: everything but the
+            // KSW youngest (the next trial's first-tile operands; none in the last trial, where
+            // vmcnt(KSW) still leaves only this trial's second-tile loads, already waited for)
+            barrier_vm<KSW>();
         } else {
             spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
         }
@@ -271,9 +287,14 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 eacc[i] += acc;
             }
         }
-        barrier_lds();                                     // s rows complete, slice read for good (LDS
+        if constexpr (SPEC) {
+            if (bn < b1 && nc > 0)
+                stage_slice(x + ((size_t)bn * C + c0) * T, nc, T, RS, LP, sm + ((bn - b0) & 1) * g.CPC * RS, tid, wave, lane);
+        } else {
+            barrier_lds();                                 // s rows complete, slice read for good (LDS
                                                            // only: no stores of this trial are out yet)
-        if (bn < b1 && nc > 0) stage_slice(x + ((size_t)bn * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
+            if (bn < b1 && nc > 0) stage_slice(x + ((size_t)bn * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
+        }
         if (row_on) {
             const float* row = Ss + wave * RS;
             // this wave's s row -> the s plane [B][F2][T], its v octets -> the v plane [B][F2][8 NO]
@@ -298,10 +319,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 for (int t = lane; t < T; t += 64) srow[t] = row[LP + t];
             }
         }
-        // next slice staged (its DMA precedes this trial's s / v stores: vmcnt is in order), s rows
-        // free; at cfg5 the SV_ST stores stay in flight into the next trial
-        if constexpr (SPEC) barrier_vm<SV_ST>();
-        else barrier_vm<0>();
+        // next slice staged, s rows free (the generic geometry: one slice and one s buffer)
+        if constexpr (!SPEC) barrier_vm<0>();
     }
 
     // ---- workgroup reduction -> one partial row (other chunks' Sv / Sv2 entries are zero) ----
