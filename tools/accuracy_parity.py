@@ -316,6 +316,43 @@ def main():
         print(f"seed {seed}: HIP {np.mean(hip[seed]):.2f}% ({time.perf_counter() - t0:.1f} s)", flush=True)
     ref = {}
     import queue as _queue
+    import signal
+
+    def _stop(signum, frame):                 # the call's time limit: keep what finished (below)
+        raise KeyboardInterrupt
+    signal.signal(signal.SIGTERM, _stop)
+    try:
+        _collect(jobs, q, procs, ref, t_start, hip, args)
+    except KeyboardInterrupt:
+        print(f"  stopped with {len(ref)}/{len(jobs)} reference units: recording those", flush=True)
+        for p in procs:
+            p.kill()
+    done_seeds = [sd for sd in args.seeds if all((sd, u) in ref for u in range(n_units))]
+    res["complete"] = len(ref) == len(jobs)
+    pairs = []
+    for seed in args.seeds:
+        us = [u for u in range(n_units) if (seed, u) in ref]
+        if not us:
+            continue
+        r = [ref[(seed, u)] for u in us]
+        h = [hip[seed][u] for u in us]
+        res["runs"].append({"seed": seed, "units": us, "hip": h, "ref": r, "hip_mean": float(np.mean(h)),
+                            "ref_mean": float(np.mean(r)), "diff_pt": float(np.mean(h) - np.mean(r))})
+        pairs += list(zip(h, r))
+    res["complete_seeds"] = done_seeds
+    res["hip_mean"] = float(np.mean([h for h, _ in pairs]))
+    res["ref_mean"] = float(np.mean([r for _, r in pairs]))
+    res.update(summarize(pairs))
+    res["within_1pt"] = bool(-1.0 <= res["ci95_pt"][0] and res["ci95_pt"][1] <= 1.0)
+    res["wall_s"] = round(time.perf_counter() - t_start, 1)
+    print(json.dumps({k: v for k, v in res.items() if k != "runs"}), flush=True)
+    if args.out:
+        with open(args.out, "w") as fo:
+            json.dump(res, fo, indent=1)
+
+
+def _collect(jobs, q, procs, ref, t_start, hip, args):
+    import queue as _queue
     for i in range(len(jobs)):
         waited = 0
         while True:                           # a heartbeat line a minute: a silent run reads as hung
@@ -329,7 +366,7 @@ def main():
                 if waited >= 3000 or not any(p.is_alive() for p in procs):
                     raise RuntimeError("reference workers stopped without a result")
         ref[(seed, u)] = acc
-        print(f"  reference unit seed {seed} #{u}: {acc:.2f}% in {secs:.1f} s", flush=True)
+        print(f"  reference unit seed {seed} #{u}: {acc!r}% in {secs:.1f} s", flush=True)
         if i % 8 == 7 or i == len(jobs) - 1:
             print(f"  reference {i + 1}/{len(jobs)} units ({time.perf_counter() - t_start:.0f} s, "
                   f"last {secs:.1f} s)", flush=True)
@@ -340,22 +377,6 @@ def main():
                                "elapsed_s": round(time.perf_counter() - t_start, 1)}, fo)
     for p in procs:
         p.join(timeout=120)
-    pairs = []
-    for seed in args.seeds:
-        r = [ref[(seed, u)] for u in range(n_units)]
-        h = hip[seed]
-        res["runs"].append({"seed": seed, "hip": h, "ref": r, "hip_mean": float(np.mean(h)),
-                            "ref_mean": float(np.mean(r)), "diff_pt": float(np.mean(h) - np.mean(r))})
-        pairs += list(zip(h, r))
-    res["hip_mean"] = float(np.mean([h for h, _ in pairs]))
-    res["ref_mean"] = float(np.mean([r for _, r in pairs]))
-    res.update(summarize(pairs))
-    res["within_1pt"] = bool(-1.0 <= res["ci95_pt"][0] and res["ci95_pt"][1] <= 1.0)
-    res["wall_s"] = round(time.perf_counter() - t_start, 1)
-    print(json.dumps({k: v for k, v in res.items() if k != "runs"}), flush=True)
-    if args.out:
-        with open(args.out, "w") as fo:
-            json.dump(res, fo, indent=1)
 
 
 if __name__ == "__main__":
