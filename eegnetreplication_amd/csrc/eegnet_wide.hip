@@ -482,6 +482,22 @@ __device__ __forceinline__ void b2_stage(const float* __restrict__ src, int F2, 
     }
 }
 
+// cfg5 (F2 = 64, T1 = 128, 512 threads): one trial's [F2][T1] block-2 plane is 4 float4 per thread --
+// loaded into registers a trial ahead (b2_pf_load) and stored into the padded LDS rows at the top of
+// the trial (b2_pf_store), instead of a synchronous b2_stage whose load latency every trial waited
+constexpr int B2PF = 4;
+__device__ __forceinline__ void b2_pf_load(const float* __restrict__ src, floatx4 (&v)[B2PF], int tid) {
+#pragma unroll
+    for (int j = 0; j < B2PF; ++j) v[j] = reinterpret_cast<const floatx4*>(src)[tid + 512 * j];
+}
+__device__ __forceinline__ void b2_pf_store(const floatx4 (&v)[B2PF], int RB, float* dst, int tid) {
+#pragma unroll
+    for (int j = 0; j < B2PF; ++j) {
+        const int i = tid + 512 * j, o = i >> 5, q = i & 31;     // TQ1 = 32 float4 per row
+        lds_st4(dst + o * RB + LQW + 4 * q, v[j]);
+    }
+}
+
 // the inverse: padded LDS rows [F2P][RB] -> trial b's [F2][T1] rows of a global plane
 __device__ __forceinline__ void b2_put(const float* src, int F2, int T1, int RB, float* __restrict__ dst, int tid,
                                        int nth) {
@@ -604,10 +620,19 @@ __global__ __launch_bounds__(NT) void k_wpass_b2(Geo gin, const float* __restric
     stage_w3(g, prm, W3s, F2P, tid, NT);
     const B2Map mp = b2_map(NJT, wave, NT / 64);
     float sr[4] = {0.f, 0.f, 0.f, 0.f}, sr2[4] = {0.f, 0.f, 0.f, 0.f};
+    constexpr bool PF = SPEC && NT == 512;             // cfg5: d2 rows a trial ahead in registers
+    floatx4 pd2[PF ? B2PF : 1];
+    if constexpr (PF)
+        if ((int)blockIdx.x < g.B) b2_pf_load(d2g + (size_t)blockIdx.x * F2 * T1, pd2, tid);
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid, NT);
+        if constexpr (PF) {
+            b2_pf_store(pd2, RB, D2, tid);
+            if (b + (int)gridDim.x < g.B) b2_pf_load(d2g + (size_t)(b + gridDim.x) * F2 * T1, pd2, tid);
+        } else {
+            b2_stage(d2g + (size_t)b * F2 * T1, F2, T1, RB, D2, tid, NT);
+        }
         __syncthreads();
         b2_dw16(D2, W2s, Q, F2, T1, RB, tid, NT);
         __syncthreads();
@@ -731,10 +756,19 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo gin, const float* __restrict
     float sdz[4] = {0.f, 0.f, 0.f, 0.f}, sdzx[4] = {0.f, 0.f, 0.f, 0.f};
     float bacc[NCLS] = {0.f, 0.f, 0.f, 0.f}, lossacc = 0.f;
     const float invB = 1.0f / (float)g.Bn;
+    constexpr bool PF = SPEC && NT == 512;             // cfg5: r rows a trial ahead in registers
+    floatx4 pr[PF ? B2PF : 1];
+    if constexpr (PF)
+        if ((int)blockIdx.x < g.B) b2_pf_load(r3g + (size_t)blockIdx.x * F2 * T1, pr, tid);
     __syncthreads();
     drain_prologue_loads();
     for (int b = blockIdx.x; b < g.B; b += gridDim.x) {
-        b2_stage(r3g + (size_t)b * F2 * T1, F2, T1, RB, XH, tid, NT);       // r rows (pass B / B2)
+        if constexpr (PF) {                                                  // r rows (pass B2)
+            b2_pf_store(pr, RB, XH, tid);
+            if (b + (int)gridDim.x < g.B) b2_pf_load(r3g + (size_t)(b + gridDim.x) * F2 * T1, pr, tid);
+        } else {
+            b2_stage(r3g + (size_t)b * F2 * T1, F2, T1, RB, XH, tid, NT);   // r rows (pass B / B2)
+        }
         __syncthreads();
         {
             float mu[4], inv[4];
