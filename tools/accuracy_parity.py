@@ -319,6 +319,7 @@ def main():
     import signal
 
     def _stop(signum, frame):                 # the call's time limit: keep what finished (below)
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)   # once: the workers' group may get it too
         raise KeyboardInterrupt
     signal.signal(signal.SIGTERM, _stop)
     try:
@@ -326,7 +327,10 @@ def main():
     except KeyboardInterrupt:
         print(f"  stopped with {len(ref)}/{len(jobs)} reference units: recording those", flush=True)
         for p in procs:
-            p.kill()
+            try:
+                p.kill()
+            except Exception:                 # already gone
+                pass
     done_seeds = [sd for sd in args.seeds if all((sd, u) in ref for u in range(n_units))]
     res["complete"] = len(ref) == len(jobs)
     pairs = []
