@@ -1097,11 +1097,6 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
         pace_prio(b - b0, b1 - b0);
-        // this trial's x rows for the dws GEMM: the buffer's last reader, the previous trial's GEMM,
-        // finished before the previous closing barrier, so the DMA goes out first thing and has the
-        // dy2 phase, the lag correlation and the FIR^T to land (issued after the dy2 phase it left
-        // ~2,300 shader cycles per trial waiting at the first barrier, profiles/r4d_timeline.txt)
-        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
         float vc[MO][8];
         if constexpr (VPF) {
 #pragma unroll
@@ -1156,6 +1151,9 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                 }
             }
         }
+        // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
+        // GEMM); they land during the lag correlation / FIR^T, by the next barrier
+        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 2, tph_);
         {
             float tl[K1];
