@@ -530,9 +530,45 @@ __device__ void adam_slice(const Geo& g, const FinArgs& fa, int part, int nparts
 
 // after pass E: spatial grad (+ clamp, model.py:44), BN1 grads, temporal-conv grad; then Adam
 constexpr int APT = 8;            // Adam elements per finalize thread: nparam <= APT * blockDim
+// fin5's one batch of global loads -- statistics, coefficients, the Adam state of its elements --
+// as registers (Fin5Stage).  k_pass_e issues it in every workgroup BEFORE the reduction ticket, so the
+// winner starts fin5 with its inputs in hand instead of one more global round trip on the critical path
+// (2.3 µs in the r4f timeline); the losers drop it.  Nothing read here changes during the pass: the
+// statistics and coefficients are the earlier finalizes', [0, o_w2) and the own slice are written only
+// by this finalize, the gradients >= o_g2 by fin3 / fin4, the step counter by fin5 at its very end.
 // own_slice >= 0: this workgroup's adam_slice (of gridDim.x) joins the staged Adam elements
-__device__ void fin5(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa,
-                     int own_slice = -1) {
+struct Fin5Stage {
+    Stage<3, double> s0;
+    Stage<3, float> s2;
+    float ap[APT], am[APT], av[APT], ag[APT];
+    int step0;
+};
+__device__ __forceinline__ void fin5_load(const Geo& g, const FinArgs& fa, int own_slice, Fin5Stage& st) {
+    const int nth = blockDim.x, tid = threadIdx.x;
+    const bool adam = fa.adam_m != nullptr;
+    const bool early = adam_early(g, fa);
+    const int na = early ? g.o_w2 : g.nparam;
+    int si0 = 0, si1 = 0;
+    if (early && own_slice >= 0) adam_slice_range(g, own_slice, gridDim.x, si0, si1);
+    const int ne = na + (si1 - si0);
+    auto pidx = [&](int e) { return e < na ? e : si0 + (e - na); };
+    st.s0.load(fa.stats, g.F1 * g.K1 + g.K1);
+    st.s2.load(fa.coef, CF_COUNT * CSTR);
+    if (adam) {   // parameters, moments and the earlier finalizes' gradients (indices >= o_g2)
+        const int last = ne - 1;
+#pragma unroll
+        for (int j = 0; j < APT; ++j) {
+            if (nth * j >= ne) break;     // block-uniform: only the batches that hold elements
+            const int i = pidx(min(tid + nth * j, last));
+            st.ap[j] = fa.params[i]; st.am[j] = fa.adam_m[i]; st.av[j] = fa.adam_v[i]; st.ag[j] = fa.grads[i];
+        }
+    }
+    st.step0 = adam ? *fa.step : 0;
+}
+// PRE: st already holds fin5_load's batch (k_pass_e); otherwise fin5 loads it here
+template <bool PRE>
+__device__ __forceinline__ void fin5_body(const Geo& g, const float* prm, const double* sums, double* scr,
+                                          const FinArgs& fa, int own_slice, Fin5Stage& st) {
     const int tid = threadIdx.x, nth = blockDim.x, K1 = g.K1, F1 = g.F1;
     double* Gw = scr;                 // (G w1)[filter][tap] (F1*K1) + S1 (K1), fin1's, from fa.stats
     double* S1 = Gw + F1 * K1;
@@ -544,7 +580,6 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     const double* Xm = sums + g.QR * K1;
     const double* Sdy = Xm + g.F2 * g.C;
     const double* Sdyv = Sdy + g.F2;
-    // ---- one batch of global loads: statistics, taps, coefficients, Adam state ----
     const bool adam = fa.adam_m != nullptr;
     const bool early = adam_early(g, fa);
     const int na = early ? g.o_w2 : g.nparam;     // [o_w2, nparam): pass E's workgroups (adam_slice)
@@ -552,31 +587,19 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
     if (early && own_slice >= 0) adam_slice_range(g, own_slice, gridDim.x, si0, si1);
     const int ne = na + (si1 - si0);
     auto pidx = [&](int e) { return e < na ? e : si0 + (e - na); };
-    float ap[APT], am[APT], av[APT], ag[APT];
-    int step0;
+    if constexpr (!PRE) fin5_load(g, fa, own_slice, st);
+    float* const ap = st.ap;
+    float* const am = st.am;
+    float* const av = st.av;
+    const float* const ag = st.ag;
+    const int step0 = st.step0;
     float es0 = 0.f, es1 = 0.f;
-    {
-        Stage<3, double> s0;
-        Stage<3, float> s2;
-        s0.load(fa.stats, F1 * K1 + K1);
-        s2.load(fa.coef, CF_COUNT * CSTR);
-        if (adam) {   // parameters, moments and the earlier finalizes' gradients (indices >= o_g2)
-            const int last = ne - 1;
-#pragma unroll
-            for (int j = 0; j < APT; ++j) {
-                if (nth * j >= ne) break;     // block-uniform: only the batches that hold elements
-                const int i = pidx(min(tid + nth * j, last));
-                ap[j] = fa.params[i]; am[j] = fa.adam_m[i]; av[j] = fa.adam_v[i]; ag[j] = fa.grads[i];
-            }
-        }
-        step0 = adam ? *fa.step : 0;
-        if (early) {                  // adam_scalars_publish (pass E, workgroup 0), in this batch
-            es0 = ld_pub(fa.coef + CF_ADAM * CSTR);
-            es1 = ld_pub(fa.coef + CF_ADAM * CSTR + 1);
-        }
-        s0.store(Gw, F1 * K1 + K1);
-        s2.store(cf, CF_COUNT * CSTR);
+    if (early) {                      // adam_scalars_publish (pass E, workgroup 0), after the ticket
+        es0 = ld_pub(fa.coef + CF_ADAM * CSTR);
+        es1 = ld_pub(fa.coef + CF_ADAM * CSTR + 1);
     }
+    st.s0.store(Gw, F1 * K1 + K1);
+    st.s2.store(cf, CF_COUNT * CSTR);
     __syncthreads();
     TRACE_FS(g, fa.tpass, 4);
     for (int p = tid; p < g.F2 * g.C; p += nth) {
@@ -647,6 +670,11 @@ __device__ void fin5(const Geo& g, const float* prm, const double* sums, double*
         fa.params[i] = pp; fa.adam_m[i] = mm; fa.adam_v[i] = vv;
     }
     if (tid == 0) *fa.step = s;
+}
+__device__ __forceinline__ void fin5(const Geo& g, const float* prm, const double* sums, double* scr,
+                                     const FinArgs& fa, int own_slice = -1) {
+    Fin5Stage st;
+    fin5_body<false>(g, prm, sums, scr, fa, own_slice, st);
 }
 
 // One pass's finalize as its own one-workgroup launch (eegnet_train_stage: synchronised-BatchNorm data

@@ -1426,8 +1426,13 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         pub(row + (QR * K1 + p), a);
     }
     double* dsm = (double*)sm;
+    // fin5's inputs, loaded before the ticket by every workgroup (the winner's are in hand when it
+    // starts fin5; eegnet_finalize.hip Fin5Stage).  Not for a deferred (synchronised-BN) pass: its
+    // k_fin runs fin5.
+    Fin5Stage f5;
+    if (!g.defer) fin5_load(g, fa, blockIdx.x, f5);
     if (grid_reduce(g, part, g.nE, fa, dsm)) {
-        fin5(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa, blockIdx.x);
+        fin5_body<true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa, blockIdx.x, f5);
         TRACE(g, 4, TR_FIN);
     } else {
         adam_slice(g, fa, blockIdx.x, gridDim.x, step0);  // off the critical path: the winner is still reducing
