@@ -213,8 +213,20 @@ __host__ __device__ constexpr int fin5_scratch_doubles(int K1, int F1, int ng) {
 // matrix-vector products G w1 as (filter, tap) lanes with four partial chains, and the filters' sums
 // over taps from LDS -- no shuffle scans.  G w1 and S1 go to fa.stats for fin5 (dW1 needs exactly those,
 // the same parameters being in force through pass E).
-template <int K1>
-__device__ void fin1(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
+// fin1's one batch of global loads (w1 | g1 | b1 | ws and the BN running statistics) as registers:
+// k_pass_a issues it in every workgroup before the reduction ticket (as k_pass_e does fin5's).  The
+// parameters change only in the previous step's fin5, the running statistics only in fin1 itself.
+struct Fin1Stage {
+    Stage<2, float> sp;
+    Stage<1, float> sb;
+};
+__device__ __forceinline__ void fin1_load(const Geo& g, const float* prm, const FinArgs& fa, Fin1Stage& st) {
+    st.sp.load(prm + g.o_w1, g.F1 * g.K1 + 2 * g.F1 + g.F2 * g.C);
+    if (fa.update_running) st.sb.load(fa.bn, 2 * g.F1 + 2 * g.F2);
+}
+template <int K1, bool PRE>
+__device__ __forceinline__ void fin1_body(const Geo& g, const float* prm, const double* sums, double* scr,
+                                          const FinArgs& fa, Fin1Stage& st) {
     const int F1 = g.F1, F2 = g.F2, C = g.C, nth = blockDim.x;
     constexpr int P = (K1 - 1) / 2, R = K1 - 1 - P, NH = R * (R + 1) / 2, NTL = P * (P + 1) / 2;
     const int GS = K1 + 1;            // padded row stride of G and Ed (conflict-free column walks)
@@ -235,12 +247,9 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
     const int tid = threadIdx.x;
     {   // w1 | g1 | b1 | ws are contiguous in the parameter vector (eegnet_host.hip param layout)
         const int nl = F1 * K1 + 2 * F1 + F2 * C, nb = 2 * F1 + 2 * F2;
-        Stage<2, float> sp;
-        Stage<1, float> sb;
-        sp.load(prm + g.o_w1, nl);
-        if (fa.update_running) sb.load(fa.bn, nb);
-        sp.store(pl, nl);
-        if (fa.update_running) sb.store(pbn, nb);
+        if constexpr (!PRE) fin1_load(g, prm, fa, st);
+        st.sp.store(pl, nl);
+        if (fa.update_running) st.sb.store(pbn, nb);
     }
     TRACE_FS(g, fa.tpass, 11);
     const double* G0 = sums;
@@ -399,6 +408,12 @@ __device__ void fin1(const Geo& g, const float* prm, const double* sums, double*
             rm2[F2 + o] = (float)((1.0 - mom) * (double)pbn[2 * F1 + F2 + o] + mom * var2 * n2 / (n2 - 1.0));
         }
     }
+}
+
+template <int K1>
+__device__ __forceinline__ void fin1(const Geo& g, const float* prm, const double* sums, double* scr, const FinArgs& fa) {
+    Fin1Stage st;
+    fin1_body<K1, false>(g, prm, sums, scr, fa, st);
 }
 
 // after pass B: BN3 (model.py:71) batch statistics

@@ -605,7 +605,12 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     }
     }
     double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nA, fa, dsm)) { fin1<K1>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa); TRACE(g, 0, TR_FIN); }
+    Fin1Stage f1;                                  // fin1's inputs, before the ticket (Fin1Stage)
+    if (!g.defer) fin1_load(g, prm, fa, f1);
+    if (grid_reduce(g, part, g.nA, fa, dsm)) {
+        fin1_body<K1, true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa, f1);
+        TRACE(g, 0, TR_FIN);
+    }
 }
 
 // ================================================================================================
