@@ -155,6 +155,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                                                  const float* __restrict__ x, float* __restrict__ sg,
                                                  float* __restrict__ vg, float* __restrict__ part,
                                                  FinArgs fa) {
+    TRACE(gin, 0, TR_ENTRY);
     const Geo g = geo_w<SPEC>(gin);
     using G_ = KG<K1>;
     constexpr int LP = G_::LP;
@@ -227,6 +228,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     if constexpr (SPEC)
         if (b0 < b1) spatial_load5(x + (size_t)b0 * C * T, bv5, 0, wave, lane);
     barrier_vm<0>();                                   // the first slice landed (asm DMA: explicit vmcnt)
+    TRACE(g, 0, TR_PRO);
+    TRACE_DECL();
     drain_prologue_loads();
     // the cfg5 geometry: every wave owns a row, whose s and v stores are SV_ST wave-instructions (2 v
     // octet halves + T / 256 s pieces); the closing barrier lets exactly those stay in flight
@@ -252,10 +255,12 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
             // FIR's SV_ST stores and this trial's 2 x KSW operand loads) landed: everything but the
             // KSW youngest (the next trial's first-tile operands; none in the last trial, where
             // vmcnt(KSW) still leaves only this trial's second-tile loads, already waited for)
+            TRACE_PH(g, 0, 0, tph_);
             barrier_vm<KSW>();
         } else {
             spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
         }
+        TRACE_PH(g, 0, 1, tph_);
         for (int c = wave; c < nc; c += NWW) {
             const float* xr = Xg + c * RS + G_::OFF + li;        // xp[i - P] = row[OFF + i]
             for (int ks = 0; ks < KQ; ++ks) {
@@ -287,6 +292,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 eacc[i] += acc;
             }
         }
+        TRACE_PH(g, 0, 2, tph_);
         if constexpr (SPEC) {
             if (bn < b1 && nc > 0)
                 stage_slice(x + ((size_t)bn * C + c0) * T, nc, T, RS, LP, sm + ((bn - b0) & 1) * g.CPC * RS, tid, wave, lane);
@@ -319,9 +325,11 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 for (int t = lane; t < T; t += 64) srow[t] = row[LP + t];
             }
         }
+        TRACE_PH(g, 0, 3, tph_);
         // next slice staged, s rows free (the generic geometry: one slice and one s buffer)
         if constexpr (!SPEC) barrier_vm<0>();
     }
+    TRACE_LOOP(g, 0);
 
     // ---- workgroup reduction -> one partial row (other chunks' Sv / Sv2 entries are zero) ----
     float* row = part + (size_t)blockIdx.x * g.nA;
@@ -1196,6 +1204,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                                                  const float* __restrict__ x, const float* __restrict__ sg,
                                                  const float* __restrict__ vg, const float* __restrict__ dp2g,
                                                  float* __restrict__ part, FinArgs fa) {
+    TRACE(gin, 4, TR_ENTRY);
     const Geo g = geo_w<SPEC>(gin);
     using G_ = KG<K1>;
     constexpr int LP = G_::LP;
@@ -1276,6 +1285,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
     __syncthreads();                                       // zero fill before the first rows land
     if (b0 < b1) { stage_rows(b0); vload(b0, vpf); }
     barrier_vm<0>();
+    TRACE(g, 4, TR_PRO);
+    TRACE_DECL();
     drain_prologue_loads();
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
@@ -1317,6 +1328,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                 }
             }
         }
+        TRACE_PH(g, 4, 0, tph_);
         wave_lds_fence();                                  // dy row complete, dp2 row read
         if (row_on) {                                      // lag correlation of this wave's row
             const float* dyr = Dys + wave * RS + LP + li;
@@ -1335,6 +1347,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                 }
             }
         }
+        TRACE_PH(g, 4, 1, tph_);
         if (row_on) {                                      // e = FIR^T(dy) -> over this wave's dy row
             const float* dyr = Dys + wave * RS;
             float e[MOW][8];
@@ -1386,9 +1399,11 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                 }
             }
         };
+        TRACE_PH(g, 4, 2, tph_);
         if (gemm_on && kg0 < kg1) xload(kg0);
         if (bn < b1) stage_rows(bn);                       // the next trial's s / dp2 rows of this wave
         barrier_lds();                                     // e rows complete
+        TRACE_PH(g, 4, 3, tph_);
         if (gemm_on) {
             const float* arow = Dys + li * RS + LP + 4 * lk;
             for (int kgs = kg0; kgs < kg1; kgs += XPF) {   // (one batch at cfg5: 8 k-groups per wave)
@@ -1407,11 +1422,14 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                 if (kgs + XPF < kg1) xload(kgs + XPF);
             }
         }
+        TRACE_PH(g, 4, 4, tph_);
         // no second barrier: the next trial writes the other dy / e buffer (this one is rewritten two
         // trials on, after the next trial's barrier, which every wave passes only once its GEMM here
         // is done); its s / dp2 rows are this wave's own, so the wave waits for its own DMAs only
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        TRACE_PH(g, 4, 5, tph_);
     }
+    TRACE_LOOP(g, 4);
     __syncthreads();
 
     // ---- reductions ----

@@ -26,13 +26,15 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--C", type=int, default=22)
     ap.add_argument("--T", type=int, default=256)
+    ap.add_argument("--F1", type=int, default=8)
+    ap.add_argument("--D", type=int, default=2)
     ap.add_argument("--dump", default=None, help="save the raw stamp array (.npy)")
     args = ap.parse_args()
     from eegnetreplication_amd import EEGNet, FusedTrainer, _lib
     lib = _lib.load()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = EEGNet(args.C, args.T, p=0.5).to(dev).train()
+    model = EEGNet(args.C, args.T, F1=args.F1, D=args.D, p=0.5).to(dev).train()
     rng = np.random.default_rng(1234)
     x = torch.from_numpy(rng.standard_normal((args.batch, args.C, args.T), dtype=np.float32)).to(dev)
     y = torch.from_numpy(rng.integers(0, 4, args.batch)).to(dev)
@@ -51,14 +53,18 @@ def main():
         np.save(args.dump, a)
     grids = [int((a[p, :, 0] > 0).sum()) for p in range(5)]
     grid = grids[0]
-    t0 = a[0, :grid, 0].min()
+    t0 = min(a[p, :grids[p], 0].min() for p in range(5) if grids[p])
     us = lambda v: (v - t0) / 100.0   # 100 MHz wall clock -> µs from pass A's first entry
     prev_end = None
     ntr = max(1, args.batch // grid)
     print(f"grids {grids} workgroups")
     for p in range(5):
+        if not grids[p]:                      # (the wide step stamps passes A and E only)
+            continue
         st = a[p, :grids[p]]
-        ntr = max(1, args.batch // grids[p])
+        F2 = args.F1 * args.D                 # the wide streaming passes: NOC o-chunk workgroups per trial
+        noc = (F2 + 15) // 16 if F2 > 16 else 1
+        ntr = max(1, args.batch * noc // grids[p])
         ent, pro, loop, pub = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
         grp = st[:, 4][st[:, 4] > 0]
         top = st[:, 5][st[:, 5] > 0]
