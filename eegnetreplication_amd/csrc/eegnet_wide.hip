@@ -219,14 +219,10 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
             ea[i] = -2;
         }
     }
-    // cfg5: the B operands of this wave's first spatial tile of the next trial (the second tile's
-    // are loaded at the top of the trial and land behind the first tile's MFMAs; holding both across
-    // the FIR spilled 10 VGPRs)
+    // cfg5: the B operands of this wave's two spatial tiles, loaded at the top of the trial
     float bv5[SPEC ? KSW : 1], bw5[SPEC ? KSW : 1];
     __syncthreads();                                   // zero fill done before the first slice lands
     if (b0 < b1 && nc > 0) stage_slice(x + ((size_t)b0 * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
-    if constexpr (SPEC)
-        if (b0 < b1) spatial_load5(x + (size_t)b0 * C * T, bv5, 0, wave, lane);
     barrier_vm<0>();                                   // the first slice landed (asm DMA: explicit vmcnt)
     TRACE(g, 0, TR_PRO);
     TRACE_DECL();
@@ -234,6 +230,20 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     // the cfg5 geometry: every wave owns a row, whose s and v stores are SV_ST wave-instructions (2 v
     // octet halves + T / 256 s pieces); the closing barrier lets exactly those stay in flight
     constexpr int SV_ST = 2 + 512 / 256;
+    // cfg5: the s / v plane stores of trial bd (v octet in vd, s row still in its LDS buffer), issued
+    // at the top of the next trial (below)
+    float vd[8];
+    int bd = -1;
+    auto plane_stores = [&](int bb) {
+        const float* rowp = sm + 2 * g.CPC * RS + ((bb - b0) & 1) * 16 * RS + wave * RS;
+        float* vrow = vg + ((size_t)bb * F2 + o) * (8 * NO);
+        __builtin_nontemporal_store((floatx4){vd[0], vd[1], vd[2], vd[3]}, reinterpret_cast<floatx4*>(vrow + 8 * lane));
+        __builtin_nontemporal_store((floatx4){vd[4], vd[5], vd[6], vd[7]}, reinterpret_cast<floatx4*>(vrow + 8 * lane + 4));
+        float* srow = sg + ((size_t)bb * F2 + o) * s_pitch(T);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            __builtin_nontemporal_store(lds_ld4(rowp + LP + 4 * lane + 256 * q), reinterpret_cast<floatx4*>(srow + 4 * lane + 256 * q));
+    };
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
         // cfg5: this trial's buffers.  Per trial: spatial GEMM -> s rows | barrier (s rows complete,
@@ -245,18 +255,20 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
         if constexpr (SPEC) {
             Xg = sm + ((b - b0) & 1) * g.CPC * RS;
             Ss = sm + 2 * g.CPC * RS + ((b - b0) & 1) * 16 * RS;
+            spatial_load5(x + (size_t)b * C * T, bv5, 0, wave, lane);
             spatial_load5(x + (size_t)b * C * T, bw5, 1, wave, lane);
+            // the previous trial's s / v plane stores go out after this trial's operand loads, so
+            // waiting for those loads (vmcnt is in order) does not wait for the stores to drain: at
+            // cfg5 the planes are 256 KB per trial and their drain was what the trial's first phase
+            // waited for (profiles/r4k_timeline_cfg5.txt; the registers of a trial-ahead operand
+            // prefetch now hold the deferred v octet)
+            if (bd >= 0) plane_stores(bd);
             spatial_mfma5(bv5, awl, Ss, RS, LP, 0, wave, lane);
-            // the next trial's first-tile operands: in flight over the second tile, the lag-Gram and
-            // the FIR
-            if (bn < b1) spatial_load5(x + (size_t)bn * C * T, bv5, 0, wave, lane);
             spatial_mfma5(bw5, awl, Ss, RS, LP, 1, wave, lane);
-            // s rows complete; this trial's slice (DMA'd in the previous trial, before the previous
-            // FIR's SV_ST stores and this trial's 2 x KSW operand loads) landed: everything but the
-            // KSW youngest (the next trial's first-tile operands; none in the last trial, where
-            // vmcnt(KSW) still leaves only this trial's second-tile loads, already waited for)
+            // s rows complete; this trial's slice (DMA'd in the previous trial, before the operand
+            // loads) landed: everything but the SV_ST youngest (the deferred stores)
             TRACE_PH(g, 0, 0, tph_);
-            barrier_vm<KSW>();
+            barrier_vm<SV_ST>();
         } else {
             spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
         }
@@ -306,6 +318,14 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
             // this wave's s row -> the s plane [B][F2][T], its v octets -> the v plane [B][F2][8 NO]
             // (passes B and E read them instead of recomputing the spatial GEMM and the FIR)
             float* vrow = vg + ((size_t)b * F2 + o) * (8 * NO);
+            if constexpr (SPEC) {                          // one octet per lane; stored next trial
+                float w[4 * G_::NW8];
+                lds_window<G_::NW8>(row + 8 * lane, w);
+                fir8<K1, G_::OFF>(w, tap, vd);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) { svl += vd[i]; sv2l = fmaf(vd[i], vd[i], sv2l); }
+                bd = b;
+            } else
             for (int oc = lane; oc < NO; oc += 64) {
                 float w[4 * G_::NW8];
                 lds_window<G_::NW8>(row + 8 * oc, w);
@@ -318,6 +338,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
                 __builtin_nontemporal_store((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
             }
             float* srow = sg + ((size_t)b * F2 + o) * s_pitch(T);
+            if constexpr (SPEC) { (void)srow; } else
             if ((T & 3) == 0) {
                 for (int t = 4 * lane; t < T; t += 256)
                     __builtin_nontemporal_store(lds_ld4(row + LP + t), reinterpret_cast<floatx4*>(srow + t));
@@ -329,6 +350,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
         // next slice staged, s rows free (the generic geometry: one slice and one s buffer)
         if constexpr (!SPEC) barrier_vm<0>();
     }
+    if constexpr (SPEC)
+        if (bd >= 0) plane_stores(bd);                    // the last trial's planes
     TRACE_LOOP(g, 0);
 
     // ---- workgroup reduction -> one partial row (other chunks' Sv / Sv2 entries are zero) ----
