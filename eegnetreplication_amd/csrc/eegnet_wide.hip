@@ -1353,6 +1353,14 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         }
         TRACE_PH(g, 4, 0, tph_);
         wave_lds_fence();                                  // dy row complete, dp2 row read
+        // cfg5: the next trial's dp2 row of this wave now (its only reader, the dy2 phase, is done) and
+        // its s row after the lag correlation -- not both after the FIR^T: the dws GEMM's x-operand
+        // wait (vmcnt is in order, and the compiler, not seeing the asm DMAs, waits for zero) then
+        // waited for DMAs issued just before it (profiles/r4k_timeline_cfg5.txt: 6.8 K cycles)
+        if constexpr (SPEC)
+            if (bn < b1 && row_on)
+                for (int p = 0; p < (T1 >> 6); ++p)
+                    dma4(dp2g + ((size_t)bn * F2 + o) * T1 + 64 * p + lane, DP + wave * T1 + 64 * p);
         if (row_on) {                                      // lag correlation of this wave's row
             const float* dyr = Dys + wave * RS + LP + li;
             const float* sr = Ss + wave * RS + G_::OFF + li;
@@ -1370,6 +1378,12 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                 }
             }
         }
+        if constexpr (SPEC)
+            if (bn < b1 && row_on) {
+                wave_lds_fence();                          // the lag correlation's s-row reads are done
+                for (int p = 0; p < (T >> 8); ++p)
+                    dma16(sg + ((size_t)bn * F2 + o) * s_pitch(T) + 256 * p + 4 * lane, Ss + wave * RS + LP + 256 * p);
+            }
         TRACE_PH(g, 4, 1, tph_);
         if (row_on) {                                      // e = FIR^T(dy) -> over this wave's dy row
             const float* dyr = Dys + wave * RS;
@@ -1424,7 +1438,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         };
         TRACE_PH(g, 4, 2, tph_);
         if (gemm_on && kg0 < kg1) xload(kg0);
-        if (bn < b1) stage_rows(bn);                       // the next trial's s / dp2 rows of this wave
+        if (!SPEC && bn < b1) stage_rows(bn);              // the next trial's s / dp2 rows of this wave
         barrier_lds();                                     // e rows complete
         TRACE_PH(g, 4, 3, tph_);
         if (gemm_on) {
