@@ -1,7 +1,10 @@
 """Merge accuracy_parity.py result files of one protocol / dropout mode run in chunks (fold subsets,
 seed subsets: one gpurun call each) into one record with the paired statistics over all units.
 
-    python tools/acc_merge.py OUT.json IN1.json IN2.json ...
+    python tools/acc_merge.py OUT.json IN1.json IN2.json[:SEED,SEED...] ...
+
+A ":0,1" suffix keeps only those seeds' runs of that input (a seed cut off by a time limit and rerun
+whole in another chunk).
 """
 import json
 import os
@@ -14,13 +17,24 @@ from accuracy_parity import summarize  # noqa: E402
 
 
 def main():
-    out, ins = sys.argv[1], sys.argv[2:]
+    out, args = sys.argv[1], sys.argv[2:]
+    ins, keep = [], []
+    for a in args:
+        path, _, seeds = a.partition(":")
+        ins.append(path)
+        keep.append({int(x) for x in seeds.split(",")} if seeds else None)
     recs = [json.load(open(p)) for p in ins]
     keys = {(r["epochs"], r["dropout"], r["protocol"].split(",")[0]) for r in recs}
     assert len(keys) == 1, f"mixed runs: {keys}"
-    pairs, runs, folds = [], [], []
-    for r, p in zip(recs, ins):
+    pairs, runs, folds, seen = [], [], [], set()
+    for r, p, k in zip(recs, ins, keep):
         for run in r["runs"]:
+            if k is not None and run["seed"] not in k:
+                continue
+            for u in run["units"]:
+                key = (r["protocol"], run["seed"], u)
+                assert key not in seen, f"unit merged twice: {key}"
+                seen.add(key)
             runs.append(dict(run, source=os.path.basename(p)))
             pairs += list(zip(run["hip"], run["ref"]))
         folds.append(r["protocol"])
