@@ -51,7 +51,7 @@ def test_train_step_matches_reference(name):
     opt.zero_grad()
     (loss * m["loss_scale"]).backward()
     assert_close(logits.detach().cpu().numpy(), g.z["logits"], name="logits")
-    assert abs(float(loss) - float(g.z["loss"])) <= 1e-4 * max(1.0, abs(float(g.z["loss"])))
+    assert abs(float(loss.detach()) - float(g.z["loss"])) <= 1e-4 * max(1.0, abs(float(g.z["loss"])))
     assert_grads_close({k: p.grad.cpu().numpy() for k, p in model.named_parameters()},
                        g.group("grad"), prefix="grad.", unclamped_scale=g.unclamped_scale())
     bufs = {k: b.cpu().numpy() for k, b in model.named_buffers()}
