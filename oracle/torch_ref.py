@@ -93,6 +93,30 @@ class TorchRefEEGNet:
     __call__ = forward
 
 
+def init_state(C: int, T: int, F1: int = 8, D: int = 2, K1: int = 32) -> dict:
+    """The reference's initial state_dict: its modules constructed in model.py:22-84's order with
+    torch.nn defaults (kaiming-uniform conv / linear weights, uniform linear bias, BN gamma 1, beta 0,
+    running 0 / 1), drawing from torch's global generator exactly as EEGNet() does -- so
+    ``torch.manual_seed(s); init_state(...)`` equals the reference's (and the product's) EEGNet(...)
+    state after the same seed, without importing either (tools/accuracy_parity.py reference workers).
+    Only the modules with parameters draw; ELU / pool / dropout / flatten draw nothing."""
+    import torch.nn as nn
+    F2 = F1 * D
+    mods = [("temporal.0", nn.Conv2d(1, F1, kernel_size=(1, K1), padding="same", bias=False)),
+            ("temporal.1", nn.BatchNorm2d(F1)),
+            ("spatial", nn.Conv2d(F1, F2, kernel_size=(C, 1), padding="valid", groups=F1, bias=False)),
+            ("aggregation.0", nn.BatchNorm2d(F2)),
+            ("block_2.0", nn.Conv2d(F2, F2, kernel_size=(1, 16), padding="same", groups=F2, bias=False)),
+            ("block_2.1", nn.Conv2d(F2, F2, kernel_size=(1, 1), padding="same", bias=False)),
+            ("block_2.2", nn.BatchNorm2d(F2)),
+            ("classifier", nn.Linear(F2 * (T // 32), 4, bias=True))]
+    state = {}
+    for pre, m in mods:
+        for k, v in m.state_dict().items():
+            state[f"{pre}.{k}"] = v.detach().clone()
+    return state
+
+
 def make_optimizer(model: TorchRefEEGNet, lr=1e-3, eps=1e-7):
     return torch.optim.Adam(model.parameters(), lr=lr, eps=eps, foreach=None, fused=None)
 

@@ -68,3 +68,17 @@ def test_torch_oracle_matches_golden(name):
     loss, logits = tr.train_step(ref, opt, torch.from_numpy(g.x), torch.from_numpy(g.y), masks)
     assert_close(logits.detach().numpy(), g.z["logits"], name="logits")
     assert_params_close({k: v.detach().numpy() for k, v in ref.params.items()}, g.group("step1"))
+
+
+@pytest.mark.parametrize("C,T,F1,D", [(22, 257, 8, 2), (22, 256, 8, 2), (64, 512, 16, 4)])
+def test_reference_init_restatement_equals_eegnet_init(C, T, F1, D):
+    """oracle/torch_ref.init_state (the accuracy tool's reference workers build their initial weights
+    with it, without importing the product package) draws what EEGNet() draws after the same seed."""
+    from eegnetreplication_amd.model import EEGNet
+    torch.manual_seed(11)
+    a = tr.init_state(C, T, F1, D)
+    torch.manual_seed(11)
+    b = EEGNet(C, T, F1, D).state_dict()
+    assert list(a) == list(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k

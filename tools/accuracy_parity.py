@@ -129,17 +129,16 @@ def device_masks(B, F2, T, seed, step, p, dev):
 def run_reference(spec, epochs, dev, common):
     """model.py:101-189 + evaluate_model on the stock-ATen restatement (fp32)."""
     from eegnetreplication_amd.dataset import epoch_permutation
-    from eegnetreplication_amd.model import EEGNet
     from oracle import torch_ref as tr
     X, y, tr_ids, va_ids, te, p, seed = spec
-    torch.manual_seed(seed)
-    init = EEGNet(C=X.shape[1], T=X.shape[2], p=p)
-    ref = tr.TorchRefEEGNet({k: v.numpy() for k, v in init.state_dict().items()}, p=p, device=dev)
+    torch.manual_seed(seed)                  # the HIP unit's EEGNet() draws the same initial weights
+    init = tr.init_state(C=X.shape[1], T=X.shape[2])
+    ref = tr.TorchRefEEGNet({k: v.numpy() for k, v in init.items()}, p=p, device=dev)
     opt = tr.make_optimizer(ref)
     gen = torch.Generator().manual_seed(seed)
     Xt = torch.as_tensor(X[tr_ids], dtype=torch.float32, device=dev)
     yt = torch.as_tensor(y[tr_ids], dtype=torch.int64, device=dev)
-    F2, T = init.F1 * init.D, X.shape[2]
+    F2, T = init["spatial.weight"].shape[0], X.shape[2]
     step = 0
     for _ in range(epochs):
         ref.training = True
@@ -175,19 +174,18 @@ def run_reference_graphed(spec, epochs, dev, common):
     read in the graph through a device step counter; the epoch's permutation copied into the graph's
     static buffer before each replay.  The first epoch runs eagerly (Adam's state is created lazily)."""
     from eegnetreplication_amd.dataset import epoch_permutation
-    from eegnetreplication_amd.model import EEGNet
     from oracle import torch_ref as tr
     import torch.nn.functional as F
     X, y, tr_ids, va_ids, te, p, seed = spec
-    torch.manual_seed(seed)
-    init = EEGNet(C=X.shape[1], T=X.shape[2], p=p)
-    ref = tr.TorchRefEEGNet({k: v.numpy() for k, v in init.state_dict().items()}, p=p, device=dev)
+    torch.manual_seed(seed)                  # the HIP unit's EEGNet() draws the same initial weights
+    init = tr.init_state(C=X.shape[1], T=X.shape[2])
+    ref = tr.TorchRefEEGNet({k: v.numpy() for k, v in init.items()}, p=p, device=dev)
     opt = torch.optim.Adam(ref.parameters(), lr=1e-3, eps=1e-7, capturable=True)
     gen = torch.Generator().manual_seed(seed)
     Xt = torch.as_tensor(X[tr_ids], dtype=torch.float32, device=dev)
     yt = torch.as_tensor(y[tr_ids], dtype=torch.int64, device=dev)
     n = len(yt)
-    F2, T = init.F1 * init.D, X.shape[2]
+    F2, T = init["spatial.weight"].shape[0], X.shape[2]
     T1, T2 = T // 4, (T // 4) // 8
     nsteps = -(-n // 64)
     keys = None
@@ -245,17 +243,33 @@ def run_reference_graphed(spec, epochs, dev, common):
     return 100.0 * float((out.argmax(1).cpu() == torch.as_tensor(te[1])).float().mean())
 
 
+def _hip_lib_mapped() -> bool:
+    """Whether this process has libeegnet_hip*.so mapped (/proc/self/maps)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return any("libeegnet_hip" in line for line in f)
+    except OSError:
+        return False
+
+
 def _worker(wid, jobs, protocol, cs_folds, epochs, common, q, graphed=True):
-    """Reference units (seed, unit index) -> (seed, unit, accuracy); specs regenerated here."""
+    """Reference units (seed, unit index) -> (seed, unit, accuracy); specs regenerated here.
+
+    A reference worker runs stock ATen ops only: its initial weights come from the oracle's
+    restatement of the reference's module construction (oracle/torch_ref.init_state), so nothing in
+    it imports the product's model or loads libeegnet_hip.so -- checked from /proc/self/maps at start
+    and after every unit and reported with each result (round-4 VERDICT item 3)."""
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
+    q.put(("info", wid, {"maps_lib_at_start": _hip_lib_mapped(), "pid": os.getpid(),
+                         "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}))
     cache = {}
     for seed, u in jobs:
         if seed not in cache:
             cache = {seed: specs_for(protocol, seed, cs_folds)}
         t0 = time.perf_counter()
         acc = (run_reference_graphed if graphed else run_reference)(cache[seed][u], epochs, dev, common)
-        q.put((seed, u, acc, time.perf_counter() - t0))
+        q.put((seed, u, acc, time.perf_counter() - t0, _hip_lib_mapped()))
 
 
 def t_crit_95(df):
@@ -284,6 +298,10 @@ def main():
                     default=[10 * s + r for s in range(9) for r in range(2)],
                     help="0-based cross-subject fold indices (default: repeats 1-2 of every subject)")
     ap.add_argument("--workers", type=int, default=8, help="reference worker processes on the GPU")
+    ap.add_argument("--worker-hw-queues", type=int, default=1,
+                    help="GPU_MAX_HW_QUEUES of each reference worker (one stream each: round 4 ran 15 "
+                         "workers at HIP's default 4, 60+ user queues on one GPU, and lost one to an "
+                         "illegal-instruction fault in a stock fill kernel)")
     ap.add_argument("--ref-eager", action="store_true",
                     help="train the reference units step by step (no CUDA graph; the original driver)")
     ap.add_argument("--out", type=str, default="")
@@ -304,8 +322,18 @@ def main():
     procs = [ctx.Process(target=_worker, args=(w, jobs[w::nw], args.protocol, args.cs_folds, args.epochs,
                                                 common, q, not args.ref_eager)) for w in range(nw)]
     t_start = time.perf_counter()
+    # the workers inherit the environment at spawn: their HIP runtime reads GPU_MAX_HW_QUEUES at init
+    saved_q = os.environ.get("GPU_MAX_HW_QUEUES")
+    os.environ["GPU_MAX_HW_QUEUES"] = str(args.worker_hw_queues)
     for p in procs:
         p.start()
+    if saved_q is None:
+        os.environ.pop("GPU_MAX_HW_QUEUES", None)
+    else:
+        os.environ["GPU_MAX_HW_QUEUES"] = saved_q
+    res["workers"] = nw
+    res["worker_hw_queues"] = args.worker_hw_queues
+    res["worker_info"] = {}
     hip = {}
     for seed in args.seeds:                   # the HIP units meanwhile, in this process
         specs = specs_for(args.protocol, seed, args.cs_folds)
@@ -322,6 +350,8 @@ def main():
         signal.signal(signal.SIGTERM, signal.SIG_IGN)   # once: the workers' group may get it too
         raise KeyboardInterrupt
     signal.signal(signal.SIGTERM, _stop)
+    args.worker_info = res["worker_info"]
+    args.worker_lib_mapped = False
     try:
         _collect(jobs, q, procs, ref, t_start, hip, args)
     except KeyboardInterrupt:
@@ -331,6 +361,8 @@ def main():
                 p.kill()
             except Exception:                 # already gone
                 pass
+    res["worker_lib_mapped"] = args.worker_lib_mapped or any(
+        i.get("maps_lib_at_start") for i in res["worker_info"].values())
     done_seeds = [sd for sd in args.seeds if all((sd, u) in ref for u in range(n_units))]
     res["complete"] = len(ref) == len(jobs)
     pairs = []
@@ -361,7 +393,14 @@ def _collect(jobs, q, procs, ref, t_start, hip, args):
         waited = 0
         while True:                           # a heartbeat line a minute: a silent run reads as hung
             try:
-                seed, u, acc, secs = q.get(timeout=60)
+                msg = q.get(timeout=60)
+                if msg[0] == "info":             # a worker's start record, not a result
+                    args.worker_info[msg[1]] = msg[2]
+                    print(f"  worker {msg[1]}: {msg[2]}", flush=True)
+                    continue
+                seed, u, acc, secs, mapped = msg
+                if mapped:
+                    args.worker_lib_mapped = True
                 break
             except _queue.Empty:
                 waited += 60
