@@ -98,6 +98,40 @@ def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
     }
 
 
+# waves per SIMD each kernel's launch configuration admits (workgroup size x workgroups per CU / 4 SIMDs)
+LAUNCH_WAVES_PER_SIMD = {"k_pass_a": 4, "k_pass_b": 4, "k_pass_c": 4, "k_pass_d": 2, "k_pass_e": 4,
+                         "k_infer": 4, "k_wpass_a": 4, "k_wpass_b": 4, "k_wpass_b2": 2, "k_wpass_c": 2,
+                         "k_wpass_d": 2, "k_wpass_e": 4, "k_infer_bf16_cfg5": 4, "k_step": 4}
+
+
+def load_util():
+    """profiles/pmc_util.json (tools/summarize_profile.py): occupancy and VALU utilisation per kernel
+    from the committed rocprofv3 SQ / GRBM counters."""
+    path = os.path.join(ROOT, "profiles", "pmc_util.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return {}
+
+
+def util_fields(name):
+    """The roofline line's occupancy / VALU fields for kernel ``name`` (north_star: "achieved HBM GB/s
+    and occupancy"), from the committed PMC passes; None where that kernel was not profiled."""
+    u = load_util().get(name)
+    if not u:
+        return {"occupancy": None, "valu_util": None}
+    lim = LAUNCH_WAVES_PER_SIMD.get(name)
+    occ = {"waves_per_simd": u["waves_per_simd"], "launch_bound_waves_per_simd": lim,
+           "frac": round(u["waves_per_simd"] / lim, 4) if lim else None,
+           "def": "4 SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs): mean resident waves per SIMD over the launch",
+           "source": u["source"]}
+    valu = {"busy_simd": u.get("valu_busy_simd"), "of_wave_cycles": u.get("valu_of_wave"),
+            "wait_over_active": u.get("wait_over_active"), "lds_bank_conflict": u.get("lds_bank_conflict"),
+            "def": "busy_simd = 4 SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs); of_wave_cycles = "
+                   "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES", "source": u["source"]}
+    return {"occupancy": occ, "valu_util": valu}
+
+
 def roofline_entry(name, fl, by_alg, by_impl, avg_s, traffic=None):
     """Roofline of one kernel, SURVEY 8(d): t_F = implemented FLOPs / FP32 peak (vector == f32
     MFMA on gfx950), t_B = algorithmic bytes (x reads) / HBM peak; the larger is the bound and
@@ -122,6 +156,7 @@ def roofline_entry(name, fl, by_alg, by_impl, avg_s, traffic=None):
     # the same launch against the other roof, for reference
     e["fp32_frac"] = round(t_f / avg_s, 4)
     e["hbm_frac_alg"] = round(t_b / avg_s, 4)
+    e.update(util_fields(name))
     return {k: e[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")} | e
 
 
@@ -357,6 +392,103 @@ def cpu_baselines(C, T, B, steps):
     return cpu, real_out
 
 
+def cpu_eval(B, C, T, F1, D, steps, threads):
+    """Reference eval forward on CPU (model.py:156-168 / evaluate_model model.py:191-227 after
+    model.eval(): running statistics, no dropout), stock ATen via oracle/torch_ref.py, fp32 (the CPU
+    bf16 eval of cfg5 asks for 68.7 GB: SURVEY 6).  Trials/s at the median of ``steps`` timed batches
+    after one warm-up; returns (trials/s, seconds)."""
+    from oracle import torch_ref as tr
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch.manual_seed(0)
+        ref = tr.TorchRefEEGNet({k: v.numpy() for k, v in tr.init_state(C, T, F1, D).items()}, p=0.5)
+        ref.training = False
+        x = torch.from_numpy(np.random.default_rng(1234).standard_normal((B, C, T), dtype=np.float32))
+        times = []
+        with torch.no_grad():
+            ref(x)
+            for _ in range(steps):
+                t0 = time.perf_counter()
+                ref(x)
+                times.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    return B / float(np.median(times)), float(sum(times))
+
+
+def cpu_train_wide(B, C, T, F1, D, steps, threads):
+    """Reference train step (fwd + CE + bwd + clamps + Adam, model.py:141-148) of EEGNet-F1,D on CPU,
+    stock ATen via oracle/torch_ref.py; trials/s at the median of ``steps`` timed steps after one
+    warm-up; returns (trials/s, seconds)."""
+    from oracle import torch_ref as tr
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        torch.manual_seed(0)
+        ref = tr.TorchRefEEGNet({k: v.numpy() for k, v in tr.init_state(C, T, F1, D).items()}, p=0.5)
+        opt = tr.make_optimizer(ref)
+        x = torch.from_numpy(np.random.default_rng(1234).standard_normal((B, C, T), dtype=np.float32))
+        y = torch.from_numpy(np.random.default_rng(1235).integers(0, 4, B))
+        tr.train_step(ref, opt, x, y)
+        times = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            tr.train_step(ref, opt, x, y)
+            times.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    return B / float(np.median(times)), float(sum(times))
+
+
+def cpu_legs(fn, sample, threads_list):
+    """Run a CPU baseline at each thread count; the best leg is the value."""
+    legs = []
+    for th in dict.fromkeys(threads_list):
+        v, secs = fn(th)
+        legs.append({"value": round(v, 1), "cores": th, "seconds": round(secs, 2)})
+    best = max(legs, key=lambda e: e["value"])
+    return {"value": best["value"], "unit": "trials/s", "cores": best["cores"], "kind": "port",
+            "sample": sample, "legs": legs}
+
+
+def bench_infer_fp32(dev, B, C, T, steps, warmup, nx=4):
+    """fp32 eval forward of EEGNet-8,2 at cfg2's shape (k_infer: the validation loop model.py:156-168
+    and evaluate_model model.py:191-227 after train() left the model in eval mode, model.py:151),
+    x rotating over ``nx`` distinct batches already in HBM.  Roofline on SURVEY 8(d)'s BN-folded
+    inference FLOPs and bytes (x once, logits out)."""
+    from eegnetreplication_amd import EEGNet, _lib
+    torch.manual_seed(1)
+    m = EEGNet(C, T, F1=8, D=2, p=0.5).to(dev).eval()
+    with torch.no_grad():
+        for name, b in m.named_buffers():
+            if name.endswith("running_var"):
+                b.uniform_(0.5, 1.5)
+    g = torch.Generator(device=dev).manual_seed(3)
+    xs = [torch.randn(B, C, T, device=dev, generator=g) for _ in range(nx)]
+    with torch.no_grad():
+        for i in range(warmup):
+            m(xs[i % nx])
+        _lib.profile_enable(True)
+        m(xs[0])
+        torch.cuda.synchronize()
+        _lib.profile_collect()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            out = m(xs[i % nx])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        kern = _lib.profile_collect()
+        _lib.profile_enable(False)
+    cnt, tot = kern.get("k_infer", (0, 0.0))
+    avg_s = tot / max(cnt, 1) * 1e-3
+    fl, by = INFER_FLOP(C, T, 16), 4 * C * T + 16
+    roof = roofline_entry("k_infer", fl * B, 4 * C * T * B, by * B, avg_s, None) if cnt else None
+    return {"metric": "fp32 eval trials/sec EEGNet-8,2 22ch x 256 (k_infer)", "value": round(B * steps / dt, 1),
+            "unit": "trials/s", "batch": B, "steps": steps, "x_buffers": nx,
+            "finite": bool(torch.isfinite(out).all()), "roofline": roof}
+
+
 INFER_BF16_BYTES = lambda C, T: 2 * C * T + 16          # bf16 x in, fp32 logits out, per trial
 # BN-folded inference FLOPs per trial (SURVEY 8(d)): spatial GEMM + FIR + dw16 + pw + classifier
 INFER_FLOP = lambda C, T, F2, K1=32: 2 * (F2 * C * T + F2 * T * K1 + F2 * (T // 4) * 16
@@ -561,7 +693,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--no-infer", action="store_true", help="skip the cfg5 bf16 inference leg")
+    ap.add_argument("--no-infer", action="store_true", help="skip the inference legs (cfg5 bf16, cfg2 fp32)")
     ap.add_argument("--infer-batch", type=int, default=16384)
     ap.add_argument("--no-folds", action="store_true", help="skip the fold-batched real-protocol leg")
     ap.add_argument("--folds", type=int, default=90,
@@ -643,6 +775,30 @@ def main():
         cfg5 = None
         if not args.no_cfg5:
             cfg5 = bench_train_cfg5(dev, args.cfg5_batch, steps=10, warmup=3)
+        eval2 = None
+        if not args.no_infer:
+            eval2 = bench_infer_fp32(dev, B, C, T, steps=20, warmup=3)
+        if not args.no_cpu_baseline and world == 1:
+            many = min(16, len(os.sched_getaffinity(0)))
+            if eval2 is not None:
+                eval2["cpu_baseline"] = cpu_legs(
+                    lambda th: cpu_eval(B, C, T, 8, 2, 3, th),
+                    f"eval forward (running statistics, no dropout) of B={B} x {C}x{T}, EEGNet-8,2, fp32: 3 timed "
+                    f"batches per leg after 1 warm-up, trials/s at the median batch; oracle/torch_ref.py on "
+                    f"stock ATen", (1, many))
+            if cfg5 is not None:
+                cfg5["cpu_baseline"] = cpu_legs(
+                    lambda th: cpu_train_wide(256, 64, 512, 16, 4, 2, th),
+                    "train steps (fwd+CE+bwd+clamps+Adam) of EEGNet-16,4 at B=256 x 64x512, fp32: 2 timed steps "
+                    "per leg after 1 warm-up (a bounded sample of the B=1024 workload: the reference's "
+                    "[B,16,64,512] conv1 activations are 0.5 GB per 256 trials), trials/s at the median step; "
+                    "oracle/torch_ref.py on stock ATen", (1, many))
+            if infer is not None:
+                infer["cpu_baseline"] = cpu_legs(
+                    lambda th: cpu_eval(512, 64, 512, 16, 4, 2, th),
+                    "fp32 eval forward of EEGNet-16,4 at B=512 x 64x512 (BASELINE.md section 3's cfg5 CPU "
+                    "workload; the CPU bf16 eval asks for 68.7 GB, SURVEY 6): 2 timed batches per leg after "
+                    "1 warm-up, trials/s at the median batch; oracle/torch_ref.py on stock ATen", (1, many))
         out = {
             "metric": "train trials/sec (fwd+bwd) EEGNet-8,2 22ch x 256",
             "value": round(trials_per_s, 1),
@@ -677,6 +833,7 @@ def main():
             "cfg4_dp": cfg4,
             "cfg5_train": cfg5,
             "cfg5_infer_bf16": infer,
+            "cfg2_eval_fp32": eval2,
             "real_protocol_folds": folds,
         }
         print(json.dumps(out), flush=True)

@@ -21,9 +21,11 @@ _lib = None
 class Fold(ctypes.Structure):
     """Mirror of ``eegnet_fold`` (include/eegnet_abi.h): one model of a fold-indexed step."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("params", "bn_buffers", "num_batches_tracked", "x", "labels",
-                                              "grads", "adam_state", "step", "losses", "ws", "perm",
-                                              "xstat")] + \
-               [("seed", ctypes.c_uint64)]
+                                              "grads", "adam_state", "step", "losses", "ws", "perm")] + \
+               [("seed", ctypes.c_uint64), ("xstat", ctypes.c_void_p)]
+
+
+ABI_VERSION = 5     # include/eegnet_abi.h EEGNET_ABI_VERSION: the struct layouts these mirrors follow
 
 
 class Dims(ctypes.Structure):
@@ -73,6 +75,7 @@ _SIGS = {
     "eegnet_x_stats_width": (ctypes.c_int, [ctypes.POINTER(Dims)]),
     "eegnet_x_stats": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.c_int64, _vp, _vp, _vp]),
     "eegnet_fold_bytes": (ctypes.c_size_t, []),
+    "eegnet_abi_version": (ctypes.c_int, []),
     "eegnet_last_error": (ctypes.c_char_p, []),
     "eegnet_build_info": (ctypes.c_char_p, []),
 }
@@ -96,6 +99,9 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.eegnet_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{p} has struct ABI {lib.eegnet_abi_version()}, this binding {ABI_VERSION}: "
+                               f"rebuild it")
         for name, mirror in (("eegnet_dims_bytes", Dims), ("eegnet_fold_bytes", Fold)):
             if getattr(lib, name)() != ctypes.sizeof(mirror):
                 raise RuntimeError(f"{p} was built with another {mirror.__name__} layout ({name}() = "
@@ -131,7 +137,7 @@ def workspace_bytes(d: Dims) -> int:
 
 KERNEL_IDS = ("k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e", "k_adam", "k_infer",
               "memset_tickets", "k_infer_bf16", "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c",
-              "k_wpass_d", "k_wpass_e", "k_winfer", "k_coltail")
+              "k_wpass_d", "k_wpass_e", "k_winfer", "k_coltail", "k_xstats")
 
 
 def profile_enable(on: bool = True, kernels=None):

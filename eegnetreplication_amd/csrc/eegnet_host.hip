@@ -151,7 +151,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     const int rows1 = g->C * g->RS;                   // x rows (one buffer)
     const int nf4 = rup(g->NF, 4);
     const bool spec = g->C == 22 && (g->T == 256 || g->T == 257) && g->F1 == 8 && g->D == 2 && g->K1 == 32;   // EEG_DISPATCH
-    g->ldsA = (spec ? 2 : 1) * rows1 + g->F2 * g->RS + NWB * (g->K1 + 1);   // compile-time shapes: two x buffers
+    // compile-time shapes: two x buffers, and two xstat-row slots (fold launches, eegnet_fold.xstat)
+    g->ldsA = (spec ? 2 : 1) * rows1 + g->F2 * g->RS + NWB * (g->K1 + 1) + (spec ? 2 * rup(g->K1 + 1 + g->nedge, 4) : 0);
     g->ldsB = 3 * g->F2 * g->RS2 + F2MAX * (K2 + F2MAX);
     // passes C / D: one trial stream per wave, each with its own block-2 rows (row_stride_b2)
     g->RSW = row_stride_b2(g->T1);
@@ -285,11 +286,11 @@ static void set_key(Geo* g, uint64_t seed, uint64_t offset) {
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
 enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_INFER_BF16,
-                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_CTAIL, KID_COUNT };
+                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_CTAIL, KID_XSTATS, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
                                               "k_adam", "k_infer", "memset_tickets", "k_infer_bf16",
                                               "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c", "k_wpass_d",
-                                              "k_wpass_e", "k_winfer", "k_coltail"};
+                                              "k_wpass_e", "k_winfer", "k_coltail", "k_xstats"};
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { unsigned mask = 0; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
@@ -1027,8 +1028,11 @@ int eegnet_x_stats(const eegnet_dims* dims, int64_t n, const float* x, float* ou
     if (lds > (size_t)LDS_MAX) return fail(EEGNET_EINVAL, "eegnet_x_stats: dims need %zu B of LDS", lds);
     const dim3 grid((unsigned)std::min<int64_t>(n, (int64_t)device_cus() * WGPC));
     hipStream_t s = (hipStream_t)stream;
-    if (g.K1 == 32) hipLaunchKernelGGL(k_xstats<32>, grid, dim3(NTB), lds, s, g, (long long)n, x, out);
-    else hipLaunchKernelGGL(k_xstats<64>, grid, dim3(NTB), lds, s, g, (long long)n, x, out);
+    {
+        PROF(KID_XSTATS);
+        if (g.K1 == 32) hipLaunchKernelGGL(k_xstats<32>, grid, dim3(NTB), lds, s, g, (long long)n, x, out);
+        else hipLaunchKernelGGL(k_xstats<64>, grid, dim3(NTB), lds, s, g, (long long)n, x, out);
+    }
     LAUNCH_CHECK("k_xstats");
     return 0;
 }
@@ -1062,6 +1066,7 @@ int eegnet_trace_enable(void* buf) {
 
 size_t eegnet_dims_bytes(void) { return sizeof(eegnet_dims); }
 size_t eegnet_fold_bytes(void) { return sizeof(eegnet_fold); }
+int eegnet_abi_version(void) { return EEGNET_ABI_VERSION; }
 
 size_t eegnet_trace_bytes(void) { return (size_t)8 * TR_MAXWG * TR_SLOTS * sizeof(unsigned long long); }
 

@@ -311,6 +311,25 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     float xacc[NXI];
 #pragma unroll
     for (int k = 0; k < NXI; ++k) xacc[k] = 0.f;
+    // DMA shapes: a trial's xstat row travels by LDS-DMA with its x rows, a trial ahead, into the
+    // other of two slots; the trial sums it from LDS at its top (landed by the previous closing
+    // barrier).  A global load of it would be waited for behind the next trial's asm x DMA (the
+    // compiler cannot see that DMA: a vmcnt wait for the load is vmcnt(0)).  Wave w DMAs and reads
+    // exactly the columns 64 w + NTB k + lane, so a slot is refilled only after its own readers.
+    constexpr bool XSDMA = FOLD && XDMA;
+    constexpr int NVP = (K1 + 1 + KG<K1>::R * (KG<K1>::R + 1) / 2 + KG<K1>::P * (KG<K1>::P + 1) / 2 +
+                         KG<K1>::R + KG<K1>::P + 3) & ~3;
+    float* const XSt = red + NWB * (K1 + 1);          // [2][NVP] (fold launches with xstat)
+    auto xstat_dma = [&](int bb, int slot) {
+        if (XSDMA && xst) {
+            const float* xr = xst + (size_t)fold_row(perm, row0, bb) * NV;
+#pragma unroll
+            for (int k = 0; k < NXI; ++k) {
+                const int c0 = 64 * wave + NTB * k;
+                if (c0 < NV && lane < NV - c0) dma4(xr + c0 + lane, XSt + slot * NVP + c0);
+            }
+        }
+    };
     static_assert(!LAGM || (KG<K1>::R <= 16 && KG<K1>::P <= 16), "edge Grams are one 16 x 16 tile");
     floatx4 egram = {0.f, 0.f, 0.f, 0.f};            // wave EW_H: head Gram tile, EW_T: tail
     float esum = 0.f;                                // wave EW_S: lane a < R head sum, R + u tail sum
@@ -340,6 +359,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         }
     }
     float pf[XDMA ? 1 : PF];
+    if (b0 < b1) xstat_dma(b0, 0);
     if constexpr (XDMA) {
         barrier_vm<0>();                              // the first x landed, pads and tables written
     } else {
@@ -361,16 +381,26 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
             // closing barrier, a whole trial later (one buffer gave it only the FIR: ~1,500 shader
             // cycles per trial waited for it, profiles/r4d_timeline.txt phase 4).
             Xb = sm + ((b - b0) & 1) * C * RS;
-            if (bn < b1) x_dma_asm(x + fold_row(perm, row0, bn) * (C * XP), C, T, XP, RS, LP,
-                                   sm + ((bn - b0) & 1) * C * RS, wave, lane);
+            if (XSDMA && xst) {                       // this trial's xstat row (landed), then the next's
+#pragma unroll
+                for (int k = 0; k < NXI; ++k)
+                    if (tid + NTB * k < NV) xacc[k] += XSt[((b - b0) & 1) * NVP + tid + NTB * k];
+            }
+            if (bn < b1) {
+                x_dma_asm(x + fold_row(perm, row0, bn) * (C * XP), C, T, XP, RS, LP,
+                          sm + ((bn - b0) & 1) * C * RS, wave, lane);
+                xstat_dma(bn, (bn - b0) & 1);
+            }
         }
         spatial_mfma<KS, NWB>(Xb, aw, Ss, C, F2, NT16, RS, LP, wave, lane);
         if (FOLD && xst) {
-            const float* xr = xst + (size_t)fold_row(perm, row0, b) * NV;
+            if constexpr (!XDMA) {                    // register-staged shapes: no asm DMA to wait behind
+                const float* xr = xst + (size_t)fold_row(perm, row0, b) * NV;
 #pragma unroll
-            for (int k = 0; k < NXI; ++k) {
-                const int c = tid + NTB * k;
-                if (c < NV) xacc[k] += xr[c];
+                for (int k = 0; k < NXI; ++k) {
+                    const int c = tid + NTB * k;
+                    if (c < NV) xacc[k] += xr[c];
+                }
             }
         } else if constexpr (LAGM) {
             // lag-Gram: items (c, octet), lanes of a wave on consecutive octets of one row
@@ -519,9 +549,11 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         TRACE_PH(g, 0, 3, tph_);
         // next x landed (asm DMA, issued at the top of the trial: explicit vmcnt), Ss free.  The
         // trial's s-plane stores are younger than that DMA, so the barrier lets them stay in flight:
-        // s_rows_store issues F2 s_pitch(T) / 4 / NTB float4 stores per thread -- 2 at 22 x 256, 2 or
-        // 3 at 22 x 257 (vmcnt(2) waits for the DMA either way)
-        if constexpr (XDMA) barrier_vm<2>();
+        // s_rows_store issues at least NSST = floor(F2 s_pitch(T) / 4 / NTB) float4 stores per thread
+        // (2 at 22 x 256, 2 or 3 at 22 x 257), so vmcnt(NSST) waits for the DMA whatever the shape
+        constexpr int NSST = (TT && FF) ? imax(0, (FF * (s_pitch(TT) / 4)) / NTB) : 0;
+        static_assert(NSST <= 16, "vmcnt window");
+        if constexpr (XDMA) barrier_vm<NSST>();
         else __syncthreads();                              // Xb staged, Ss free
         if constexpr (DEFER) {
             if (o < F2) {

@@ -50,7 +50,12 @@ class FoldBatch:
         same model shape for every fold, F1*D <= 16, and (per epoch) the same number of trials.
         ``xstats``: fused launches read each batch's parameter-free BN1 statistics from a per-trial
         table of every fold's X (ops.x_stats, computed once per X and refreshed when X changes in
-        place) instead of recomputing the lag-Gram from x every step."""
+        place) instead of recomputing the lag-Gram from x every step.
+
+        Change detection is PyTorch's version counter (``X._version``), which tracked in-place ops
+        bump.  Writes that bypass it -- through ``X.data``, DLPack or another library's view of the
+        storage, a ctypes / HIP kernel -- must be followed by ``invalidate_x()``: without it the
+        table (and, at 22 x 257, the padded copy the kernels read) keeps the old trials."""
         if len(models) != len(seeds) or not models:
             raise ValueError("need one seed per model and at least one model")
         dev = models[0].flat_parameters().device
@@ -73,6 +78,14 @@ class FoldBatch:
 
     def __len__(self):
         return len(self.models)
+
+    def invalidate_x(self):
+        """Recompute every fold's padded x copy and per-trial BN1 table from its X at the next epoch
+        (for writes to X that PyTorch's version counter does not see: ``X.data``, DLPack, foreign
+        kernels).  Same storage: the fold tables and the captured graph stay valid."""
+        if self._fz is not None:
+            for ent in self._fz["xsrc"].values():
+                ent["ver"] = None
 
     def _workspace(self, k, B):
         ws = self._ws[k].get(B)

@@ -272,7 +272,9 @@ def fold_table(entries, device) -> torch.Tensor:
     n = len(entries)
     arr = (_lib.Fold * n)()
     for i, e in enumerate(entries):
-        for name, _ in _lib.Fold._fields_[:-1]:
+        for name, _ in _lib.Fold._fields_:
+            if name == "seed":
+                continue
             t = e.get(name)
             setattr(arr[i], name, 0 if t is None else t.data_ptr())
         arr[i].seed = int(e["seed"]) & ((1 << 64) - 1)

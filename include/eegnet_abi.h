@@ -166,9 +166,10 @@ typedef struct eegnet_fold {
     void* ws;                       /* workspace of eegnet_workspace_bytes(dims), zeroed once     */
     const int64_t* perm;            /* epoch permutation: batch row r is x / labels row perm[r]   */
                                     /* (NULL: row r itself, i.e. x already shuffled)              */
-    const float* xstat;             /* NULL, or eegnet_x_stats(x) of this fold's x: its rows' BN1  */
-                                    /* lag sums, read instead of recomputed every epoch           */
     uint64_t seed;                  /* dropout key seed: key = mix(seed, offset + *step)          */
+    const float* xstat;             /* NULL, or eegnet_x_stats(x) of this fold's x: its rows' BN1  */
+                                    /* lag sums, read instead of recomputed every epoch (ABI 5:   */
+                                    /* appended after seed, so the round-3 fields keep offsets)   */
 } eegnet_fold;
 
 /* The hot-loop iteration of eegnet_train_step (forward + CE + backward + clamps + Adam) for
@@ -199,7 +200,7 @@ int eegnet_x_stats(const eegnet_dims* dims, int64_t n, const float* x, float* ou
 /* Optional per-kernel device timing for benchmarks: `on` is a bitmask of kernel ids (bit i = the
  * i-th name eegnet_profile_collect reports: k_pass_a, k_pass_b, k_pass_c, k_pass_d, k_pass_e,
  * k_adam, k_infer, memset_tickets, k_infer_bf16, k_wpass_a, k_wpass_b, k_wpass_b2, k_wpass_c,
- * k_wpass_d, k_wpass_e, k_winfer, k_coltail; -1 = all, 0 = off; the k_w* kernels are the F2 > 16 path).  Every selected kernel this
+ * k_wpass_d, k_wpass_e, k_winfer, k_coltail, k_xstats; -1 = all, 0 = off; the k_w* kernels are the F2 > 16 path).  Every selected kernel this
  * thread launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect
  * synchronises them and reports, per kernel name (32-byte slots in `names`), launch count and
  * summed device ms; it returns the number of kernels in *n_out.  Not for use under hipGraph
@@ -233,6 +234,14 @@ int eegnet_wide_spec(const eegnet_dims* dims);
  * fold after the first from the wrong offsets). */
 size_t eegnet_dims_bytes(void);
 size_t eegnet_fold_bytes(void);
+
+/* The struct layouts above are versioned: EEGNET_ABI_VERSION changes whenever a field of eegnet_dims
+ * or eegnet_fold moves (a reordering keeps the size, so eegnet_fold_bytes alone cannot catch it).
+ * A caller asserts eegnet_abi_version() == the EEGNET_ABI_VERSION it was compiled against.
+ *   4: eegnet_fold.xstat added before seed (round 4)
+ *   5: xstat moved after seed -- the round-3 fields at their round-3 offsets again (round 5) */
+#define EEGNET_ABI_VERSION 5
+int eegnet_abi_version(void);
 
 /* Thread-local description of the last error ("" if none). */
 const char* eegnet_last_error(void);

@@ -29,6 +29,9 @@ def test_library_exports_every_symbol():
     for name in _header_symbols():
         assert hasattr(lib, name), name
     assert b"gfx950" in lib.eegnet_build_info()
+    txt = open(os.path.join(ROOT, "include", "eegnet_abi.h")).read()
+    ver = int(re.search(r"#define EEGNET_ABI_VERSION (\d+)", txt).group(1))
+    assert lib.eegnet_abi_version() == ver == _lib.ABI_VERSION
 
 
 def test_param_count_and_validation():

@@ -361,3 +361,39 @@ def test_fold_launch_with_x_stats_matches_recomputed():
         assert_params_close({n: p.detach().cpu().numpy() for n, p in a.named_parameters()},
                             {n: p.detach().cpu().numpy() for n, p in b.named_parameters()}, steps=9,
                             rtol=1e-4, atol_frac=1e-4, prefix=f"fold {k} xstats vs recomputed ")
+
+
+@pytest.mark.parametrize("T_", [256, 257])
+def test_untracked_x_write_needs_invalidate(T_):
+    """A write to X through ``X.data`` does not bump X._version, so FoldBatch cannot see it; after
+    ``invalidate_x()`` the graphed fold launches (per-trial BN1 table, and at 22 x 257 the padded
+    copy) train on the new values -- bit for bit what a fresh FoldBatch on them trains."""
+    from eegnetreplication_amd import EEGNet, FoldBatch
+    dev = _dev()
+    rng = np.random.default_rng(41)
+    X0 = torch.from_numpy(rng.standard_normal((128, C, T_), dtype=np.float32)).to(dev)
+    X1 = torch.from_numpy(rng.standard_normal((128, C, T_), dtype=np.float32)).to(dev)
+    y = torch.from_numpy(rng.integers(0, 4, 128)).to(dev)
+    runs = []
+    for mode in ("data_write", "fresh"):
+        torch.manual_seed(9)
+        models = [EEGNet(C, T_, p=0.0).to(dev).train() for _ in range(2)]
+        fb = FoldBatch(models, [3, 4], graphs=True, fused=True, xstats=True)
+        gens = [torch.Generator().manual_seed(s) for s in (3, 4)]
+        X = X0.clone()
+        fb.epoch([(X, y)] * 2, 64, gens)
+        if mode == "data_write":
+            ver = X._version
+            X.data.copy_(X1)                         # not seen by the version counter
+            assert X._version == ver
+            fb.invalidate_x()
+            Xe = X
+        else:
+            Xe = X1.clone()
+        fb.epoch([(Xe, y)] * 2, 64, gens)
+        fb.epoch([(Xe, y)] * 2, 64, gens)
+        torch.cuda.synchronize()
+        runs.append([_state(fb, k) for k in range(2)])
+    for k in range(2):
+        for a, b in zip(runs[0][k], runs[1][k]):
+            assert torch.equal(a, b), f"fold {k}: the X.data write was not picked up after invalidate_x()"
