@@ -37,6 +37,22 @@ ALG_BYTES_PER_TRIAL = 45_056     # x read twice
 CFG4_GLOBAL_BATCH = 65536        # BASELINE configs[3]
 
 
+STEP_KERNEL = "k_step"      # the persistent step: all five passes in one launch (eegnet_persist.hip)
+
+
+def with_step_kernel(alg, ab=None):
+    """The per-pass tables plus the persistent step kernel, whose work per trial is the whole step's:
+    (sum of the passes' FLOPs, sum of their bytes); its algorithmic bytes are the step's (x twice +
+    the label).  The sums over the passes stay over ``alg`` itself."""
+    out = dict(alg)
+    out[STEP_KERNEL] = (sum(v[0] for v in alg.values()), sum(v[1] for v in alg.values()))
+    if ab is None:
+        return out
+    ab2 = dict(ab)
+    ab2[STEP_KERNEL] = sum(ab.values())
+    return out, ab2
+
+
 def kernel_alg_bytes(C=22, T=256, wide=False):
     """SURVEY 8(d)'s algorithmic HBM bytes per trial, attributed to the kernels that need them: x
     is read once for the forward (pass A) and once for the weight gradients (pass E); the labels
@@ -655,7 +671,8 @@ def bench_cfg4(dev, rank, world, G, steps, warmup, barrier, nx=2):
     for i in range(warmup):
         tr.step(xs[i % nx], ys[i % nx])
     alg = kernel_algorithmic(C, T)
-    dt, table, dom, dk = timed_steps(tr, xs, ys, steps, alg, B, barrier)
+    alg_k, ab_k = with_step_kernel(alg, kernel_alg_bytes(C, T))
+    dt, table, dom, dk = timed_steps(tr, xs, ys, steps, alg_k, B, barrier)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -664,11 +681,10 @@ def bench_cfg4(dev, rank, world, G, steps, warmup, barrier, nx=2):
     if rank != 0:
         return None
     tps = G * steps / dt
-    ab = kernel_alg_bytes(C, T)
     roof = None
     if dom and dk:
-        fl, by = alg[dom]
-        roof = roofline_entry(dom, fl * B, ab[dom] * B, by * B, dk[1] / dk[0] * 1e-3, None)
+        fl, by = alg_k[dom]
+        roof = roofline_entry(dom, fl * B, ab_k[dom] * B, by * B, dk[1] / dk[0] * 1e-3, None)
     flop = sum(v[0] for v in alg.values())
     return {"metric": "train trials/sec (fwd+CE+bwd+Adam) EEGNet-8,2 22ch x 256, data parallel",
             "value": round(tps, 1), "unit": "trials/s", "global_batch": G, "batch_per_gpu": B,
@@ -679,7 +695,7 @@ def bench_cfg4(dev, rank, world, G, steps, warmup, barrier, nx=2):
             "step_roofline": step_roofline(flop, ALG_BYTES_PER_TRIAL, sum(v[1] for v in alg.values()),
                                            tps / world),
             "hbm_fraction": round(ALG_BYTES_PER_TRIAL * tps / (PEAK_HBM_GBS * 1e9 * world), 4),
-            "kernels": kernel_table(table, alg, B, ab)}
+            "kernels": kernel_table(table, alg_k, B, ab_k)}
 
 
 def main():
@@ -736,7 +752,8 @@ def main():
     for i in range(args.warmup):
         trainer.step(xs[i % args.nx], ys[i % args.nx])
     alg = kernel_algorithmic(C, T)
-    dt, table, dom, dk = timed_steps(trainer, xs, ys, args.steps, alg, B, barrier, prof)
+    alg_k, ab_k = with_step_kernel(alg, kernel_alg_bytes(C, T))
+    dt, table, dom, dk = timed_steps(trainer, xs, ys, args.steps, alg_k, B, barrier, prof)
     loss = float(trainer.loss.item())
 
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -755,12 +772,12 @@ def main():
         folds = bench_folds(dev, args.folds, 1440, 2, rank, world, barrier)
     if rank == 0:
         ab = kernel_alg_bytes(C, T)
-        per_kernel = kernel_table(table, alg, B, ab)
+        per_kernel = kernel_table(table, alg_k, B, ab_k)
         pmc = load_pmc() if (B, C, T) == (4096, 22, 256) else {}
         roof = None
         if dom is not None and dk:
-            fl, by = alg[dom]
-            roof = roofline_entry(dom, fl * B, ab[dom] * B, by * B, dk[1] / dk[0] * 1e-3,
+            fl, by = alg_k[dom]
+            roof = roofline_entry(dom, fl * B, ab_k[dom] * B, by * B, dk[1] / dk[0] * 1e-3,
                                   pmc.get(dom, {}).get("hbm_bytes_per_launch"))
         impl_flop = sum(v[0] for v in alg.values())
         impl_bytes = sum(v[1] for v in alg.values())
@@ -818,7 +835,8 @@ def main():
                        "channels": C, "parallelism": f"dp{world}"},
             "roofline": roof,
             "step_roofline": step_roofline(impl_flop, ALG_BYTES_PER_TRIAL, impl_bytes, trials_per_s / world,
-                                           pmc_step_bytes(pmc, alg), B),
+                                           pmc.get(STEP_KERNEL, {}).get("hbm_bytes_per_launch")
+                                           if dom == STEP_KERNEL else pmc_step_bytes(pmc, alg), B),
             "cpu_baseline": cpu,
             "hbm_fraction": round(ALG_BYTES_PER_TRIAL * trials_per_s / world / (PEAK_HBM_GBS * 1e9), 4),
             "step_fp32_frac": round(impl_flop * trials_per_s / world / (PEAK_FP32_TFLOPS * 1e12), 4),

@@ -26,7 +26,9 @@ static inline size_t rupz(size_t a, size_t m) { return (a + m - 1) / m * m; }
 constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 800 B, a multiple of 16
 
 struct WsLayout {
-    size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v, q3, r3, total;
+    size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v, q3, r3;
+    size_t ptot, psync, pcoef, pstats, pgrads;   // the persistent step (k_step, eegnet_persist.hip)
+    size_t total;
 };
 
 static int device_cus() {
@@ -248,8 +250,9 @@ static WsLayout make_layout(const Geo& g) {
     L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
     L.partA = take((size_t)g.gridS * g.nA * 4);
     L.partB = take((size_t)std::max(g.gridS, g.grid) * g.nB * 4);
-    L.partC = take((size_t)std::max(g.grid, g.gridB2) * g.nC * 4);
-    L.partD = take((size_t)std::max(g.grid, g.gridB2) * g.nD * 4);
+    // (k_step runs passes C / D on the streaming grid)
+    L.partC = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridS) * g.nC * 4);
+    L.partD = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridS) * g.nD * 4);
     L.partE = take((size_t)g.gridS * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
     L.sums = take((size_t)nmax * 8 * NGRPMAX);
@@ -265,6 +268,13 @@ static WsLayout make_layout(const Geo& g) {
     // C (r) and D (q, r) instead of recomputing them from d2
     L.q3 = take(per);
     L.r3 = take(per);
+    // the persistent step: column totals, barrier words (zero-filled with the workspace, re-armed by
+    // every launch), and every workgroup's coefficient block / fin1 statistics / gradient copy
+    L.ptot = take((size_t)nmax * 8);
+    L.psync = take((size_t)PS_WORDS * 4);
+    L.pcoef = take((size_t)g.gridS * CF_COUNT * CSTR * 4);
+    L.pstats = take((size_t)g.gridS * (g.F1 * g.K1 + g.K1) * 8);
+    L.pgrads = take((size_t)g.gridS * g.nparam * 4);
     L.total = o;
     return L;
 }
@@ -286,11 +296,12 @@ static void set_key(Geo* g, uint64_t seed, uint64_t offset) {
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
 enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_INFER_BF16,
-                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_CTAIL, KID_XSTATS, KID_COUNT };
+                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_CTAIL, KID_XSTATS, KID_STEP,
+                KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
                                               "k_adam", "k_infer", "memset_tickets", "k_infer_bf16",
                                               "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c", "k_wpass_d",
-                                              "k_wpass_e", "k_winfer", "k_coltail", "k_xstats"};
+                                              "k_wpass_e", "k_winfer", "k_coltail", "k_xstats", "k_step"};
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { unsigned mask = 0; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
@@ -366,7 +377,49 @@ static void ensure_attrs() {
     hipFuncSetAttribute((const void*)k_xstats<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 22, 256, 16>();
     set_attrs_shape<32, 22, 257, 16>();
+    hipFuncSetAttribute((const void*)k_step<32, 22, 256, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    hipFuncSetAttribute((const void*)k_step<32, 22, 257, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     g_attr_done = true;
+}
+
+// ---- the persistent step (k_step, eegnet_persist.hip) ----
+// LDS (floats) of k_step: the largest phase, pass C / D re-laid for 8-wave workgroups, the grid
+// reductions with their finalize scratch (fin1 after A, fin5 after E)
+static int persist_lds(const Geo& g) {
+    const int nf4 = rup(g.NF, 4), nw = NTB / 64;
+    int l = std::max(std::max(g.ldsA, g.ldsB), g.ldsE);
+    l = std::max(l, std::max(nw * nf4, nw * g.nC));
+    l = std::max(l, std::max(pd_lds_floats(), nw * g.nD));
+    l = std::max(l, 2 * (preduce_doubles(g.nA) + fin1_scratch_doubles(g.K1, g.F1, g.F2, g.C)));
+    l = std::max(l, 2 * (preduce_doubles(g.nE) + fin5_scratch_doubles(g.K1, g.F1, g.o_g2)));
+    l = std::max(l, 16 * g.RS + 2 * preduce_doubles(g.nD));
+    l = std::max(l, 2 * (preduce_doubles(g.nC)));
+    return l;
+}
+// Whether a step of geometry g may run as k_step: the compile-time EEGNet-8,2 shapes, and a grid every
+// workgroup of which is resident at once (two per CU: the occupancy query with k_step's real
+// registers and LDS, cached per shape) -- the grid barriers need it
+static bool persist_ok(const Geo& g) {
+    if (g.wide || g.defer || g.K1 != 32 || g.C != 22 || (g.T != 256 && g.T != 257) || g.F1 != 8 || g.D != 2) return false;
+    if (g.XP != g.T) return false;                       // (the pitched 22 x 257 rows are the fold launches')
+    {   // the compile-time geometry k_step overwrites its Geo with (EEG_SHAPE_N22) must be make_geo's
+#define EEG_EQ_(f, v) && g.f == v
+        const bool same = g.T == 256 ? (true EEG_SHAPE_N256(EEG_EQ_)) : (true EEG_SHAPE_N257(EEG_EQ_));
+#undef EEG_EQ_
+        if (!same) return false;
+    }
+    if (const char* e = getenv("EEGNET_PERSIST")) if (e[0] == '0') return false;
+    static int ok[2] = {-1, -1};
+    const int i = g.T == 256 ? 0 : 1;
+    if (ok[i] < 0) {
+        const int lds = persist_lds(g) * 4;
+        int nb = 0;
+        const void* f = i == 0 ? (const void*)k_step<32, 22, 256, 16> : (const void*)k_step<32, 22, 257, 16>;
+        ensure_attrs();
+        if (lds > 80 * 1024 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, NTB, lds) != hipSuccess) nb = 0;
+        ok[i] = nb >= WGPC ? 1 : 0;
+    }
+    return ok[i] == 1 && g.gridS <= WGPC * device_cus();
 }
 
 // compile-time shape specialisations (the benchmark and real-data configurations); any other shape
@@ -846,6 +899,31 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
+    if ((flags & EEGNET_PERSIST) && persist_ok(g)) {
+        // the whole step as ONE launch of a co-resident grid (eegnet_persist.hip)
+        StepArgs a;
+        memset(&a, 0, sizeof(a));
+        a.x = x; a.labels = labels; a.params = params; a.bn = bn_buffers; a.nbt = num_batches_tracked;
+        a.grads = grads; a.adam_m = adam_state; a.adam_v = adam_state ? adam_state + g.nparam : nullptr;
+        a.step = step; a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.loss = loss; a.logits = logits;
+        a.cmode = PC_BWD | PC_CE | (logits ? PC_LOGITS : 0);
+        a.s = (float*)(w + L.s); a.v = (float*)(w + L.v); a.d2 = (float*)(w + L.d2); a.E1 = (float*)(w + L.E1);
+        a.E2 = (float*)(w + L.E2); a.q3 = (float*)(w + L.q3); a.r3 = (float*)(w + L.r3); a.dl = (float*)(w + L.dl);
+        a.dp2 = (float*)(w + L.dp2);
+        a.partA = (float*)(w + L.partA); a.partB = (float*)(w + L.partB); a.partC = (float*)(w + L.partC);
+        a.partD = (float*)(w + L.partD); a.partE = (float*)(w + L.partE);
+        a.tot = (double*)(w + L.ptot); a.sync = (unsigned*)(w + L.psync);
+        a.cnt = (unsigned*)(w + L.cnt); a.part2 = (double*)(w + L.sums);
+        a.wcoef = (float*)(w + L.pcoef); a.wstats = (double*)(w + L.pstats); a.wgrads = (float*)(w + L.pgrads);
+        const size_t lds = (size_t)persist_lds(g) * 4;
+        {
+            PROF(KID_STEP);
+            if (g.T == 256) hipLaunchKernelGGL((k_step<32, 22, 256, 16>), dim3(g.gridS), dim3(NTB), lds, s, g, a);
+            else hipLaunchKernelGGL((k_step<32, 22, 257, 16>), dim3(g.gridS), dim3(NTB), lds, s, g, a);
+        }
+        LAUNCH_CHECK("k_step");
+        return 0;
+    }
     int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s)
                        : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s);
     if (r) return r;

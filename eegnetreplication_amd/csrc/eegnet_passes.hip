@@ -142,15 +142,18 @@ __device__ __forceinline__ void bn3_rows(const float* coef, int F2, const float 
 // Per-wave LDS: Hs [NF] -- the flattened head features (model.py:75 Flatten order), then their
 // gradients.
 // ================================================================================================
-template <int K1, int CC, int TT, int FF, bool FOLD = false>
-__global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* __restrict__ prm,
-                                                const float* coef,    // the finalize writes it: no __restrict__
-                                                const float* __restrict__ r3g,
-                                                const uint8_t* __restrict__ mask3,
-                                                const float* __restrict__ dlin,
-                                                const int64_t* __restrict__ labels,
-                                                float* __restrict__ logits, float* __restrict__ dlout,
-                                                float* __restrict__ part, int mode, FinArgs fa, FoldCall fc) {
+// PERSIST (k_step): the workgroup's trials are its streaming-pass range (trial_range), dealt over its
+// waves, so the r plane rows it reads are the ones its own pass B wrote; `hook` runs before the loop
+template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST, class Hook>
+__device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restrict__ prm,
+                                            const float* coef,    // the finalize writes it: no __restrict__
+                                            const float* __restrict__ r3g,
+                                            const uint8_t* __restrict__ mask3,
+                                            const float* __restrict__ dlin,
+                                            const int64_t* __restrict__ labels,
+                                            float* __restrict__ logits, float* __restrict__ dlout,
+                                            float* __restrict__ part, int mode, FinArgs fa, const FoldCall& fc,
+                                            float* sm, const Hook& hook) {
     EEG_DIMS(g);
     TRACE(g, 2, TR_ENTRY);
     unsigned dk1;
@@ -176,7 +179,6 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     constexpr int NFQ = (TT && FF) ? (FF * (TT / 32) + 63) / 64 : MAXNFQ;
     const int NFP = rup4(NF);
     const int nw = blockDim.x >> 6;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     float* Hs = sm + wave * NFP;
@@ -195,11 +197,22 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     for (int j = 0; j < 2 * F2MAX; ++j) sdz[j] = 0.f;
     float bacc[NCLS] = {0.f, 0.f, 0.f, 0.f}, lossacc = 0.f;
     const float invB = 1.0f / (float)g.Bn;
+    int bfirst, bstop, bstep;
+    if constexpr (PERSIST) {
+        trial_range(g, bfirst, bstop);
+        bfirst += wave;
+        bstep = nw;
+    } else {
+        bfirst = blockIdx.x * nw + wave;
+        bstop = g.B;
+        bstep = gridDim.x * nw;
+    }
+    hook();                                        // (k_step: BN3's statistics of this step)
 
     TRACE(g, 2, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
-    for (int b = blockIdx.x * nw + wave; b < g.B; b += gridDim.x * nw) {
+    for (int b = bfirst; b < bstop; b += bstep) {
         float xh[F2MAX][MQ];
         {
             // block 2 up to the pointwise mix is pass B's (its r plane): BN3 normalisation only
@@ -338,8 +351,24 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     float* row = part + (size_t)blockIdx.x * g.nC;
     for (int c = tid; c < g.nC; c += blockDim.x) pub(row + c, wave_rows_sum<NTH / 64>(red, nw, g.nC, c));
     TRACE_PS(g, 11);
-    double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
+    if constexpr (!PERSIST) {
+        double* dsm = (double*)sm;
+        if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
+    }
+}
+
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
+__global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* __restrict__ prm,
+                                                const float* coef,    // the finalize writes it: no __restrict__
+                                                const float* __restrict__ r3g,
+                                                const uint8_t* __restrict__ mask3,
+                                                const float* __restrict__ dlin,
+                                                const int64_t* __restrict__ labels,
+                                                float* __restrict__ logits, float* __restrict__ dlout,
+                                                float* __restrict__ part, int mode, FinArgs fa, FoldCall fc) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    pass_c_body<K1, CC, TT, FF, FOLD, false>(g, prm, coef, r3g, mask3, dlin, labels, logits, dlout, part, mode, fa,
+                                             fc, sm, NoHook{});
 }
 
 // ================================================================================================
@@ -499,16 +528,18 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
         if (b + bstep < g.B) load_trial(b + bstep);
         // dW3[j][i] += sum_t dr[j][t] q[i][t] on the matrix cores (float4 k-permuted operands)
         {
+            // (ds_read_b64 operands, t = 16 kg + 2 lk + {0, 1}, + 8: conflict-free, as pass E's dws GEMM)
             const bool on = li < F2;
-            const float* ar = P2 + (on ? li : 0) * RSW + LPQ + 4 * lk;
-            const float* br = P1 + (on ? li : 0) * RSW + LPQ + 4 * lk;
+            const float* ar = P2 + (on ? li : 0) * RSW + LPQ + 2 * lk;
+            const float* br = P1 + (on ? li : 0) * RSW + LPQ + 2 * lk;
             for (int kg = 0; kg < nkg; ++kg) {
-                floatx4 a4 = lds_ld4(ar + 16 * kg), b4 = lds_ld4(br + 16 * kg);
-                if (!on) { a4 = (floatx4){0.f, 0.f, 0.f, 0.f}; b4 = a4; }
-                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], acc3, 0, 0, 0);
-                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], acc3, 0, 0, 0);
-                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], acc3, 0, 0, 0);
-                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], acc3, 0, 0, 0);
+                floatx2 a0 = lds_ld2(ar + 16 * kg), a1 = lds_ld2(ar + 16 * kg + 8);
+                floatx2 b0 = lds_ld2(br + 16 * kg), b1 = lds_ld2(br + 16 * kg + 8);
+                if (!on) { a0 = (floatx2){0.f, 0.f}; a1 = a0; b0 = a0; b1 = a0; }
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b0[0], acc3, 0, 0, 0);
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b0[1], acc3, 0, 0, 0);
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b1[0], acc3, 0, 0, 0);
+                acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b1[1], acc3, 0, 0, 0);
             }
         }
         wave_lds_fence();                          // q rows consumed before dq overwrites them

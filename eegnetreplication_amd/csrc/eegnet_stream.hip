@@ -232,11 +232,22 @@ __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict_
 //   hs / ts = head / tail sample sums       (window-sum corrections)
 //   Sv, Sv2 = sum v, sum v^2 per row o      (BN2: y2 = a1 v + c1 W)
 // ================================================================================================
-template <int K1, int CC, int TT, int FF, bool FOLD = false>
-__global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __restrict__ prm,
-                                                      const float* __restrict__ x, float* __restrict__ sg,
-                                                      float* __restrict__ vg, float* __restrict__ part,
-                                                      FinArgs fa, FoldCall fc) {
+// No-op prologue hook of the stand-alone pass kernels.  The persistent step kernel (k_step,
+// eegnet_persist.hip) passes one that waits for the previous phase's grid reduction and runs its
+// finalize, called where each pass first reads the coefficients -- after the first trial's data loads
+// are in flight.
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+// PERSIST: the body of one phase of the persistent step kernel (k_step): it publishes its partial row
+// and returns; k_step runs the grid reduction and the finalize.  Otherwise the stand-alone pass, which
+// ends in the ticketed reduction + finalize (grid_reduce).
+template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST>
+__device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restrict__ prm,
+                                            const float* __restrict__ x, float* __restrict__ sg,
+                                            float* __restrict__ vg, float* __restrict__ part,
+                                            FinArgs fa, const FoldCall& fc, float* sm) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     const int XP = EEG_XP(TT, g);
@@ -259,12 +270,11 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
     }
     // every pass re-arms its own tickets when it finishes; pass A also clears those of the later
     // passes of this call (stream order), so a call never depends on how the previous one ended
-    if (blockIdx.x == 0 && threadIdx.x < (TK_PASSES - 1) * NCNT)
+    if (!PERSIST && blockIdx.x == 0 && threadIdx.x < (TK_PASSES - 1) * NCNT)
         __hip_atomic_store(fa.cnt + NCNT + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     constexpr int NTS = FF ? 1 : RPW;
     constexpr int NEI = G_::template nei<NTB>();
     const int D = FF ? 2 : g.D;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr bool XDMA = TT != 0;                    // compile-time shapes: x / s rows by LDS-DMA
     // x buffers: compile-time shapes double-buffer x (trial b + 1 goes out by DMA at the top of trial
     // b, a whole trial ahead of its use); the others stage through registers into one buffer
@@ -403,10 +413,15 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
                 }
             }
         } else if constexpr (LAGM) {
-            // lag-Gram: items (c, octet), lanes of a wave on consecutive octets of one row
+            // lag-Gram: items (c, octet); a wave's 64 items are rows 2p, 2p + 1 in the FIR layout
+            // (fir_row / fir_oct): every 16-lane group of a ds_read_b128 then covers 8 octets of EACH
+            // row, 16 disjoint bank quads (rows RS = 4 mod 8 floats apart).  One row per wave, lanes on
+            // consecutive octets, put octets o and o + 8 in one group: a 2-way conflict on every
+            // window read (34 % of pass A's LDS cycles in round 4, profiles/r4m_pmc_summary.json).
             constexpr int TO = (TT + 7) / 8;
+            static_assert(TO == 32 && CC % 2 == 0, "LAGM: two rows of 32 octets per wave");
             for (int j = tid; j < CC * TO; j += NTB) {
-                const int c = j / TO, o = j - c * TO;
+                const int c = 2 * (j >> 6) + fir_row(j & 63), o = fir_oct(j & 63);
                 float w[4 * G_::NW8];
                 lds_window<G_::NW8>(Xb + c * RS + 8 * o, w);
                 float a[8];
@@ -636,13 +651,24 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
         if (ea[i] != -2 && tid + NTB * i < g.nedge) pub(row + (K1 + 1 + tid + NTB * i), eacc[i]);
     }
     }
-    double* dsm = (double*)sm;
-    Fin1Stage f1;                                  // fin1's inputs, before the ticket (Fin1Stage)
-    if (!g.defer) fin1_load(g, prm, fa, f1);
-    if (grid_reduce(g, part, g.nA, fa, dsm)) {
-        fin1_body<K1, true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa, f1);
-        TRACE(g, 0, TR_FIN);
+    if constexpr (!PERSIST) {
+        double* dsm = (double*)sm;
+        Fin1Stage f1;                              // fin1's inputs, before the ticket (Fin1Stage)
+        if (!g.defer) fin1_load(g, prm, fa, f1);
+        if (grid_reduce(g, part, g.nA, fa, dsm)) {
+            fin1_body<K1, true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa, f1);
+            TRACE(g, 0, TR_FIN);
+        }
     }
+}
+
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
+__global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __restrict__ prm,
+                                                      const float* __restrict__ x, float* __restrict__ sg,
+                                                      float* __restrict__ vg, float* __restrict__ part,
+                                                      FinArgs fa, FoldCall fc) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    pass_a_body<K1, CC, TT, FF, FOLD, false>(g, prm, x, sg, vg, part, fa, fc, sm);
 }
 
 // ================================================================================================
@@ -759,15 +785,15 @@ __global__ __launch_bounds__(NTB) void k_xstats(Geo g, long long n, const float*
 // part row: [Sr F2][Sr2 F2]
 // LDS: d2 rows (pad LP2) | q rows x 2 (alternate trials) | weight table [w2 F2MAX x 16][W3 F2MAX x F2MAX]
 // ================================================================================================
-template <int K1, int CC, int TT, int FF, bool FOLD = false>
-__global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __restrict__ prm,
-                                                      const float* coef,    // the finalize writes it: no __restrict__
-                                                      const float* __restrict__ vg,
-                                                      const uint8_t* __restrict__ mask2,
-                                                      float* __restrict__ d2g, float* __restrict__ E1g,
-                                                      float* __restrict__ E2g, float* __restrict__ q3g,
-                                                      float* __restrict__ r3g, float* __restrict__ part,
-                                                      FinArgs fa, FoldCall fc) {
+template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST, class Hook>
+__device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restrict__ prm,
+                                            const float* coef,    // the finalize writes it: no __restrict__
+                                            const float* __restrict__ vg,
+                                            const uint8_t* __restrict__ mask2,
+                                            float* __restrict__ d2g, float* __restrict__ E1g,
+                                            float* __restrict__ E2g, float* __restrict__ q3g,
+                                            float* __restrict__ r3g, float* __restrict__ part,
+                                            FinArgs fa, const FoldCall& fc, float* sm, const Hook& hook) {
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 1, TR_ENTRY);
     unsigned dk0;
@@ -786,7 +812,6 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     } else {
         dk0 = drop_key(g, 0);
     }
-    extern __shared__ __attribute__((aligned(16))) float sm[];
     float* D2s = sm;
     float* Qs0 = D2s + F2 * RS2;
     float* Wt = Qs0 + 2 * F2 * RS2;    // block-2 weights, read with wave-uniform addresses
@@ -802,6 +827,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
     constexpr bool VPF = TT != 0;
     float vpf[MO][8];
     if (VPF && b0 < b1) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
+    hook();                                        // (k_step: the coefficients of this step's BN1 / BN2)
 
     for (int i = tid; i < 3 * F2 * RS2; i += NTB) sm[i] = 0.f;     // pads stay zero
     for (int i = tid; i < F2MAX * (K2 + F2MAX); i += NTB) {
@@ -943,8 +969,24 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
             pub(row + ((k < 2 ? 0 : F2) + o), rv[0]);
         }
     }
-    double* dsm = (double*)sm;
-    if (grid_reduce(g, part, g.nB, fa, dsm)) { fin2(g, dsm + 2, fa); TRACE(g, 1, TR_FIN); }
+    if constexpr (!PERSIST) {
+        double* dsm = (double*)sm;
+        if (grid_reduce(g, part, g.nB, fa, dsm)) { fin2(g, dsm + 2, fa); TRACE(g, 1, TR_FIN); }
+    }
+}
+
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
+__global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __restrict__ prm,
+                                                      const float* coef,    // the finalize writes it: no __restrict__
+                                                      const float* __restrict__ vg,
+                                                      const uint8_t* __restrict__ mask2,
+                                                      float* __restrict__ d2g, float* __restrict__ E1g,
+                                                      float* __restrict__ E2g, float* __restrict__ q3g,
+                                                      float* __restrict__ r3g, float* __restrict__ part,
+                                                      FinArgs fa, FoldCall fc) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    pass_b_body<K1, CC, TT, FF, FOLD, false>(g, prm, coef, vg, mask2, d2g, E1g, E2g, q3g, r3g, part, fa, fc, sm,
+                                             NoHook{});
 }
 
 // ================================================================================================
@@ -956,13 +998,16 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 // Per trial: x DMA (for this trial's dws GEMM) | dy2 from v -> dy rows | lag correlation (dy, s) and
 // FIR^T (dy -> e, in place) | barrier | next trial's s / dp2 DMA and v loads | dws GEMM (e, x) | barrier
 // ================================================================================================
-template <int K1, int CC, int TT, int FF, bool FOLD = false>
-__global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,   // Adam (finalize) writes it
-                                                      const float* coef,    // the finalize writes it: no __restrict__
-                                                      const float* __restrict__ x,
-                                                      const float* __restrict__ sg, const float* __restrict__ vg,
-                                                      const float* __restrict__ dp2g,
-                                                      float* __restrict__ part, FinArgs fa, FoldCall fc) {
+// PERSIST: `hook` (k_step's wait for pass D's reduction and its finalize) runs after the first trial's
+// s / dp2 DMA and v loads are issued, with the dy / x rows (not yet written) as its LDS scratch
+template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST, class Hook>
+__device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   // Adam (finalize) writes it
+                                            const float* coef,    // the finalize writes it: no __restrict__
+                                            const float* __restrict__ x,
+                                            const float* __restrict__ sg, const float* __restrict__ vg,
+                                            const float* __restrict__ dp2g,
+                                            float* __restrict__ part, FinArgs fa, const FoldCall& fc, float* sm,
+                                            const Hook& hook) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     const int XP = EEG_XP(TT, g);
@@ -985,7 +1030,6 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
     constexpr int NTS = FF ? 1 : RPW;
     const int D = FF ? 2 : g.D;
     const int QR = FF ? FF / 2 : g.QR;           // Q rows in the partial row (EEGNet-8,2 shapes: F1)
-    extern __shared__ __attribute__((aligned(16))) float sm[];
     float* const Ss = sm;                        // s rows
     float* const Dys = Ss + F2 * RS;             // dy2 rows, then (in place) e = FIR^T(dy2)
     float* const Xb = Dys + F2 * RS;             // x rows (the dws GEMM's operand)
@@ -1096,6 +1140,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         if constexpr (VPF) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
         TRACE_PS(g, 4);
     }
+    hook();                                        // (k_step: scratch = the dy / x rows, not yet written)
     if constexpr (XDMA) zero_pads(sm, 2 * F2 + C, RS, LP, T, tid);   // the data windows are DMA'd / written
     load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
     TRACE_PS(g, 2);
@@ -1115,8 +1160,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         }
         if (lane < 8 * RPW && RPW * wave + (lane >> 3) < F2) CT[8 * RPW * wave + lane] = cv;
     }
-    adam_scalars_publish(g, fa);
-    const int step0 = adam_step0(g, fa);           // before the reduction ticket (adam_slice)
+    if constexpr (!PERSIST) adam_scalars_publish(g, fa);
+    const int step0 = PERSIST ? 0 : adam_step0(g, fa);   // before the reduction ticket (adam_slice)
     if constexpr (XDMA) barrier_vm<0>();          // first s / dp2 landed (asm DMA), pads and tables written
     else __syncthreads();
     if constexpr (!XDMA) {
@@ -1173,8 +1218,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                     sdyl += d;
                     sdyvl = fmaf(d, v, sdyvl);
                 }
-                lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
-                lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
+                lds_st_oct(drow + 8 * oc, oc, (floatx4){dy[0], dy[1], dy[2], dy[3]}, (floatx4){dy[4], dy[5], dy[6], dy[7]});
             }
         }
         TRACE_PH(g, 4, 1, tph_);
@@ -1229,8 +1273,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
 #pragma unroll
                 for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
                 wave_lds_fence();                          // every dy / s read of this wave is done
-                lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
-                lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+                lds_st_oct(erow + 8 * oc, oc, (floatx4){e[0], e[1], e[2], e[3]}, (floatx4){e[4], e[5], e[6], e[7]});
                 if constexpr (PIPEE) {                     // next trial's s rows of this wave
                     if (bn < b1) {
 #pragma unroll
@@ -1296,8 +1339,8 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                             if (oc < NO) {
 #pragma unroll
                                 for (int i = 0; i < 8; ++i) e[m][i] = (8 * oc + i < T) ? e[m][i] : 0.f;
-                                lds_st4(erow + 8 * oc, (floatx4){e[m][0], e[m][1], e[m][2], e[m][3]});
-                                lds_st4(erow + 8 * oc + 4, (floatx4){e[m][4], e[m][5], e[m][6], e[m][7]});
+                                lds_st_oct(erow + 8 * oc, oc, (floatx4){e[m][0], e[m][1], e[m][2], e[m][3]},
+                                           (floatx4){e[m][4], e[m][5], e[m][6], e[m][7]});
                             }
                         }
                     }
@@ -1319,8 +1362,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                             for (int i = 0; i < 8; ++i) e[i] = fmaf(tl[K1 - 1 - k], w[G_::OFFD + i + k], e[i]);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
-                        lds_st4(erow + 8 * oc, (floatx4){e[0], e[1], e[2], e[3]});
-                        lds_st4(erow + 8 * oc + 4, (floatx4){e[4], e[5], e[6], e[7]});
+                        lds_st_oct(erow + 8 * oc, oc, (floatx4){e[0], e[1], e[2], e[3]}, (floatx4){e[4], e[5], e[6], e[7]});
                     }
                 }
             }
@@ -1352,19 +1394,23 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
         // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
         if (gemm_on) {
+            // operands by ds_read_b64: lane lk takes t = 16 kg + 2 lk + {0, 1} and 16 kg + 8 + 2 lk +
+            // {0, 1} (the same permutation of k in A and B).  A 32-lane group then reads 16 rows x 4
+            // dwords = all 64 banks once (RS / 4 odd); the float4 form (ds_read_b128, 16-lane groups
+            // with lk = 0 and 1 rows mixed) put 7 of its 16 lanes on a busy bank quad: 2-way
             const int c = ct * 16 + li;
-            const float* arow = Eb + (li < F2 ? li : 0) * RS + LP + 4 * lk;
-            const float* brow = Xb + (c < C ? c : 0) * RS + LP + 4 * lk;
+            const float* arow = Eb + (li < F2 ? li : 0) * RS + LP + 2 * lk;
+            const float* brow = Xb + (c < C ? c : 0) * RS + LP + 2 * lk;
             const bool aon = li < F2, bon = c < C;
             for (int kg = kg0; kg < kg1; ++kg) {
-                floatx4 a4 = lds_ld4(arow + 16 * kg);
-                floatx4 b4 = lds_ld4(brow + 16 * kg);
-                if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
+                floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow + 16 * kg + 8);
+                floatx2 b0 = lds_ld2(brow + 16 * kg), b1 = lds_ld2(brow + 16 * kg + 8);
+                if (!aon) { a0 = (floatx2){0.f, 0.f}; a1 = a0; }
+                if (!bon) { b0 = (floatx2){0.f, 0.f}; b1 = b0; }
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b0[0], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b0[1], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b1[0], xacc, 0, 0, 0);
+                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b1[1], xacc, 0, 0, 0);
             }
         }
         if (bn < b1) {
@@ -1462,18 +1508,31 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
         for (int w = ct2 * wpc; w < (ct2 + 1) * wpc; ++w) a += red[w * 256 + oo2 * 16 + cc];
         pub(row + (QR * K1 + p), a);
     }
-    double* dsm = (double*)sm;
-    // fin5's inputs, loaded before the ticket by every workgroup (the winner's are in hand when it
-    // starts fin5; eegnet_finalize.hip Fin5Stage).  Not for a deferred (synchronised-BN) pass: its
-    // k_fin runs fin5.
-    Fin5Stage f5;
-    if (!g.defer) fin5_load(g, fa, blockIdx.x, f5);
-    if (grid_reduce(g, part, g.nE, fa, dsm)) {
-        fin5_body<true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa, blockIdx.x, f5);
-        TRACE(g, 4, TR_FIN);
-    } else {
-        adam_slice(g, fa, blockIdx.x, gridDim.x, step0);  // off the critical path: the winner is still reducing
+    if constexpr (!PERSIST) {
+        double* dsm = (double*)sm;
+        // fin5's inputs, loaded before the ticket by every workgroup (the winner's are in hand when it
+        // starts fin5; eegnet_finalize.hip Fin5Stage).  Not for a deferred (synchronised-BN) pass: its
+        // k_fin runs fin5.
+        Fin5Stage f5;
+        if (!g.defer) fin5_load(g, fa, blockIdx.x, f5);
+        if (grid_reduce(g, part, g.nE, fa, dsm)) {
+            fin5_body<true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nE), fa, blockIdx.x, f5);
+            TRACE(g, 4, TR_FIN);
+        } else {
+            adam_slice(g, fa, blockIdx.x, gridDim.x, step0);  // off the critical path: the winner is still reducing
+        }
     }
+}
+
+template <int K1, int CC, int TT, int FF, bool FOLD = false>
+__global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,   // Adam (finalize) writes it
+                                                      const float* coef,    // the finalize writes it: no __restrict__
+                                                      const float* __restrict__ x,
+                                                      const float* __restrict__ sg, const float* __restrict__ vg,
+                                                      const float* __restrict__ dp2g,
+                                                      float* __restrict__ part, FinArgs fa, FoldCall fc) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    pass_e_body<K1, CC, TT, FF, FOLD, false>(g, prm, coef, x, sg, vg, dp2g, part, fa, fc, sm, NoHook{});
 }
 
 }  // namespace eeg

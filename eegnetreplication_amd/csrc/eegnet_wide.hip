@@ -1346,8 +1346,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
                         sdyl += d;
                         sdyvl = fmaf(d, v, sdyvl);
                     }
-                    lds_st4(drow + 8 * oc, (floatx4){dy[0], dy[1], dy[2], dy[3]});
-                    lds_st4(drow + 8 * oc + 4, (floatx4){dy[4], dy[5], dy[6], dy[7]});
+                    lds_st_oct(drow + 8 * oc, oc, (floatx4){dy[0], dy[1], dy[2], dy[3]}, (floatx4){dy[4], dy[5], dy[6], dy[7]});
                 }
             }
         }
@@ -1410,8 +1409,8 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
             for (int m = 0; m < MOW; ++m) {
                 const int oc = lane + 64 * m;
                 if (oc < NO) {
-                    lds_st4(erow + 8 * oc, (floatx4){e[m][0], e[m][1], e[m][2], e[m][3]});
-                    lds_st4(erow + 8 * oc + 4, (floatx4){e[m][4], e[m][5], e[m][6], e[m][7]});
+                    lds_st_oct(erow + 8 * oc, oc, (floatx4){e[m][0], e[m][1], e[m][2], e[m][3]},
+                               (floatx4){e[m][4], e[m][5], e[m][6], e[m][7]});
                 }
             }
         }
@@ -1422,17 +1421,25 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         constexpr int XPF = 4;
         const int cx = ct * 16 + li;
         const bool bon = cx < C;
-        const float* xr = x + ((size_t)b * C + (bon ? cx : 0)) * T + 4 * lk;
+        // k permutation of the operands: lane lk takes t = 16 kg + 2 lk + {0, 1} and 16 kg + 8 + 2 lk +
+        // {0, 1} -- the e rows as ds_read_b64 (a 32-lane group reads 16 rows x 4 dwords, all 64 banks
+        // once; the float4 form was 2-way), x as two 8-byte loads into the same register order
+        const float* xr = x + ((size_t)b * C + (bon ? cx : 0)) * T + 2 * lk;
         floatx4 xpf[XPF];
         auto xload = [&](int kgs) {
 #pragma unroll
             for (int i = 0; i < XPF; ++i) {
-                const int kg = min(kgs + i, kg1 - 1), t0 = 16 * kg + 4 * lk;
-                if ((T & 3) == 0 && t0 + 3 < T) {
-                    xpf[i] = *reinterpret_cast<const floatx4*>(xr + 16 * kg);
+                const int kg = min(kgs + i, kg1 - 1), t0 = 16 * kg + 2 * lk;
+                if ((T & 1) == 0 && t0 + 9 < T) {
+                    const floatx2 u = *reinterpret_cast<const floatx2*>(xr + 16 * kg);
+                    const floatx2 v = *reinterpret_cast<const floatx2*>(xr + 16 * kg + 8);
+                    xpf[i] = (floatx4){u[0], u[1], v[0], v[1]};
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) xpf[i][e] = (t0 + e < T) ? xr[16 * kg + e] : 0.f;
+                    for (int e = 0; e < 4; ++e) {
+                        const int dt = (e & 1) + 8 * (e >> 1);
+                        xpf[i][e] = (t0 + dt < T) ? xr[16 * kg + dt] : 0.f;
+                    }
                 }
             }
         };
@@ -1442,18 +1449,18 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         barrier_lds();                                     // e rows complete
         TRACE_PH(g, 4, 3, tph_);
         if (gemm_on) {
-            const float* arow = Dys + li * RS + LP + 4 * lk;
+            const float* arow = Dys + li * RS + LP + 2 * lk;
             for (int kgs = kg0; kgs < kg1; kgs += XPF) {   // (one batch at cfg5: 8 k-groups per wave)
 #pragma unroll
                 for (int i = 0; i < XPF; ++i) {
                     const int kg = kgs + i;
                     if (kg < kg1) {
-                        const floatx4 a4 = lds_ld4(arow + 16 * kg);
+                        const floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow + 16 * kg + 8);
                         const floatx4 b4 = bon ? xpf[i] : (floatx4){0.f, 0.f, 0.f, 0.f};
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[0], b4[0], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[1], b4[1], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[2], b4[2], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[3], b4[3], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b4[0], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b4[1], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b4[2], xacc, 0, 0, 0);
+                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b4[3], xacc, 0, 0, 0);
                     }
                 }
                 if (kgs + XPF < kg1) xload(kgs + XPF);
