@@ -645,33 +645,61 @@ __device__ __forceinline__ void x_store(const float (&pf)[PF], int C, int T, int
 
 // spatial A operand (ws, 16 o x 4 c per k-step) kept in registers for the whole workgroup:
 // lane l holds ws[o = l&15][c = 4s + (l>>4)] for k-step s (zero outside F2 x C); KS = ceil(C/4)
+// EEGNET_LDSX_A = n (counter builds only, wrong results): drop one class of pass A's LDS accesses
+// (tools/lds_probe.sh): 1 spatial GEMM operands, 3 lag-Gram windows, 5 s-plane store reads, 6 FIR
+// windows, 7 the in-loop x DMA
+#ifndef EEGNET_LDSX_A
+#define EEGNET_LDSX_A 0
+#endif
+// the channel of MFMA k-row lk (0-3) in k-step s of the spatial GEMM.  ds_read_b32 serves each
+// 32-lane half (lk = 0, 1 | lk = 2, 3) in one cycle over 32 banks: rows c and c + 1 (RS = 4 mod 8
+// floats apart) put 16 lanes on overlapping banks, a 2-way conflict on every operand read.  Steps
+// 2j, 2j + 1 instead take channels 8j .. 8j + 7 with each half on rows c, c + 4 (4 RS = 16 mod 32:
+// disjoint banks).  Odd KS keeps the plain order.
+template <int KS>
+__device__ __forceinline__ int spatial_ch(int s, int lk) {
+    if constexpr (KS % 2 == 0) {
+        // step part (compile-time: an immediate LDS offset) + lane part (in the base address)
+        return (8 * (s >> 1) + 2 * (s & 1)) + ((lk >> 1) + 4 * (lk & 1));
+    } else {
+        return 4 * s + lk;
+    }
+}
+
 template <int KS>
 __device__ __forceinline__ void load_ws_frag(const float* __restrict__ ws, int C, int F2, float (&aw)[KS],
                                              int lane) {
     const int o = lane & 15, lk = lane >> 4;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-        const int c = 4 * s + lk;
+        const int c = spatial_ch<KS>(s, lk);
         aw[s] = (o < F2 && c < C) ? ws[o * C + c] : 0.f;
     }
 }
 
 // s[o,t] = sum_c ws[o,c] x[c,t] on the matrix cores: v_mfma_f32_16x16x4_f32, A = ws (registers),
-// B = x tile (4 c x 16 t).  Lane l: A[l&15][l>>4], B[l>>4][l&15]; D[4(l>>4)+r][l&15] (CDNA4 maps).
-// Exact f32 (a k-ordered fmaf chain).  Wave w computes column tiles w, w+16, ...
+// B = x tile (4 c x 16 t).  Lane l: A[l&15][spatial_ch(s, l>>4)], B[spatial_ch(s, l>>4)][l&15];
+// D[4(l>>4)+r][l&15] (CDNA4 maps).  Exact f32 up to the order of the channel sum.  Wave w computes
+// column tiles w, w+16, ...
 template <int KS, int NW = NWAVE>
 __device__ __forceinline__ void spatial_mfma(const float* Xs, const float (&aw)[KS], float* Ss, int C, int F2,
                                              int NT16, int RS, int LP, int wave, int lane) {
     const int li = lane & 15, lk = lane >> 4;
-    const int ks = (C + 3) >> 2;
+    int ks = (C + 3) >> 2;
+    if constexpr (KS % 2 == 0) ks = (ks + 1) & ~1;     // spatial_ch: steps 2j, 2j + 1 hold 8 channels
+    const int cl = spatial_ch<KS>(0, lk);
+    const float* xcol = Xs + LP + li + cl * RS;
     for (int n = wave; n < NT16; n += NW) {
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        const float* xcol = Xs + lk * RS + LP + 16 * n + li;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             if (s < ks) {
-                const int c = 4 * s + lk;
-                const float b = (c < C) ? xcol[4 * s * RS] : 0.f;
+                const int c = spatial_ch<KS>(s, lk), cs = c - cl;     // cs: the step's part
+#if EEGNET_LDSX_A == 1
+                const float b = 0.01f * (c + n);
+#else
+                const float b = (c < C) ? xcol[cs * RS + 16 * n] : 0.f;
+#endif
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aw[s], b, acc, 0, 0, 0);
             }
         }

@@ -20,6 +20,11 @@
 //   group's taps -- so a 64-sample chunk still fills all 16 columns.
 // * depthwise 1x16 on the matrix cores too (banded Toeplitz of the row's 16 taps, K = 32 window;
 //   8 of 16 columns used), instead of 131 K VALU FMAs per trial.
+// EEGNET_KX = n (timing builds only, wrong results; tools/infer_probe.sh): 1 no spatial GEMM, 2 no FIR
+// phase, 3 no block-2 tail, 4 no compute (DMA and barriers only), 5 no x DMA
+#ifndef EEGNET_KX
+#define EEGNET_KX 0
+#endif
 namespace eeg {
 namespace c5 {
 
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
             PH_(0);
             // ---- 1. spatial GEMM s^T[t][o] (16 t x 16 o tiles, A = x^T by transposed reads) ----
 #pragma unroll
-            for (int m = 0; m < 3; ++m) {
+            for (int m = 0; m < ((EEGNET_KX == 1 || EEGNET_KX == 4) ? 0 : 3); ++m) {
                 const int n = tt0 + 2 * m;
                 const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
                 const bf16x8 a0 = tr_frag(Xi, XROWB, 0, 16 * n, lane), a1 = tr_frag(Xi, XROWB, 32, 16 * n, lane);
@@ -224,11 +229,12 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
             PH_(1);
             barrier_lds_c();                               // s rows complete; x buffer consumed
             PH_(2);
-            if (j + 2 < NCH) x_chunk_dma(x + (size_t)b * C * T, j + 2, Xi, wave, lane);
+            if (EEGNET_KX == 5) {
+            } else if (j + 2 < NCH) x_chunk_dma(x + (size_t)b * C * T, j + 2, Xi, wave, lane);
             else if (j == NCH - 2 && more) x_chunk_dma(xn, 0, Xi, wave, lane);   // next trial's chunk 0
             // ---- 2. FIR (banded Toeplitz MFMA), folded BN, ELU, pool4 -> a rows ----
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
+            for (int q = 0; q < ((EEGNET_KX == 2 || EEGNET_KX == 4) ? 0 : 2); ++q) {
                 const int gg = 2 * wave + q;
                 const int o = D * gg + (l15 >> 2), tile = l15 & 3;
                 const char* srw = Si + o * (2 * SROW) + 2 * (16 * tile + 8 * G);
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
         // ---- 3. depthwise 1x16 (pad 7 | 8) on the matrix cores -> z image (x buffer 1) ----
         // z[o][16n + i] = sum_j A[i][j] W_n[j], A[i][j] = w2[o][j - i - 1], W_n[j] = a[o][16n + j - 8]
 #pragma unroll 4
-        for (int rr = 0; rr < F2 / NW; ++rr) {
+        for (int rr = 0; rr < ((EEGNET_KX == 3 || EEGNET_KX == 4) ? 0 : F2 / NW); ++rr) {
             const int o = wave * (F2 / NW) + rr;
             const uint16_t* wp = W2p + o * W2R + 15 + 8 * G - l15;
             bf16x8 aw;
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
         // ---- 4. pointwise MFMA (A = W3, B = z by transposed reads), BN3, ELU, pool8, classifier ----
         float lp0 = 0.f, lp1 = 0.f;                       // classes pc0, pc0 + 1 of this lane's row prr
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < ((EEGNET_KX == 3 || EEGNET_KX == 4) ? 0 : 4); ++m) {
             const int n = tt0 + 2 * m;
             floatx4 acc = {0.f, 0.f, 0.f, 0.f};
             acc = mfma_bf16(w3f[0], tr_frag(Zi, XROWB, 0, 16 * n, lane), acc);
@@ -315,7 +321,7 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
             for (int w = 0; w < NW; ++w) a += Lg[w * NCLS + tid];
             logits[(size_t)b * NCLS + tid] = a;
         }
-        if (more) x_chunk_dma(xn, 1, smc + OFF_X1, wave, lane);  // next trial's chunk 1 (x buffer 1 is free)
+        if (more && EEGNET_KX != 5) x_chunk_dma(xn, 1, smc + OFF_X1, wave, lane);  // next trial's chunk 1
         PH_(7);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

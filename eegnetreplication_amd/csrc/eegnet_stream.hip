@@ -397,8 +397,9 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
                     if (tid + NTB * k < NV) xacc[k] += XSt[((b - b0) & 1) * NVP + tid + NTB * k];
             }
             if (bn < b1) {
-                x_dma_asm(x + fold_row(perm, row0, bn) * (C * XP), C, T, XP, RS, LP,
-                          sm + ((bn - b0) & 1) * C * RS, wave, lane);
+                if (EEGNET_LDSX_A != 7)
+                    x_dma_asm(x + fold_row(perm, row0, bn) * (C * XP), C, T, XP, RS, LP,
+                              sm + ((bn - b0) & 1) * C * RS, wave, lane);
                 xstat_dma(bn, (bn - b0) & 1);
             }
         }
@@ -423,7 +424,11 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
             for (int j = tid; j < CC * TO; j += NTB) {
                 const int c = 2 * (j >> 6) + fir_row(j & 63), o = fir_oct(j & 63);
                 float w[4 * G_::NW8];
-                lds_window<G_::NW8>(Xb + c * RS + 8 * o, w);
+                if (EEGNET_LDSX_A == 3) {
+#pragma unroll
+                    for (int i = 0; i < 4 * G_::NW8; ++i) w[i] = 0.001f * (j + i);
+                } else
+                    lds_window<G_::NW8>(Xb + c * RS + 8 * o, w);
                 float a[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) a[i] = (8 * o + i < T) ? w[G_::OFF + i] : 0.f;
@@ -502,7 +507,7 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
             if (bn < b1) x_prefetch<PF, NTB>(x + fold_row(perm, row0, bn) * (C * XP), C, T, pf, tid);   // live over the FIR only
         TRACE_PH(g, 0, 1, tph_);
         // s rows -> the s plane [B][F2][T] (pass E's lag-correlation operand)
-        s_rows_store<NTB>(Ss, sg + (size_t)b * F2 * s_pitch(T), F2, T, RS, LP, tid);
+        if (EEGNET_LDSX_A != 5) s_rows_store<NTB>(Ss, sg + (size_t)b * F2 * s_pitch(T), F2, T, RS, LP, tid);
         // v = 32-tap FIR of this wave's s rows; BN2 sums of v; v -> the v plane [B][F2][8 NO] (passes
         // B and E read it back instead of recomputing the spatial GEMM and the FIR).  Compile-time
         // shapes hold v in registers across the trial's closing barrier and store it after, so the
@@ -525,7 +530,11 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
                         const int oc = fir_oct(lane) + 32 * m;
                         if (oc < NO) {
                             float w[4 * G_::NW8];
-                            lds_window<G_::NW8>(row + 8 * oc, w);
+                            if (EEGNET_LDSX_A == 6) {
+#pragma unroll
+                                for (int i = 0; i < 4 * G_::NW8; ++i) w[i] = 0.001f * (oc + i);
+                            } else
+                                lds_window<G_::NW8>(row + 8 * oc, w);
                             if (TAIL1 && m == MOA - 1) {
                                 float a = 0.f;
 #pragma unroll
@@ -1000,6 +1009,12 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 // ================================================================================================
 // PERSIST: `hook` (k_step's wait for pass D's reduction and its finalize) runs after the first trial's
 // s / dp2 DMA and v loads are issued, with the dy / x rows (not yet written) as its LDS scratch
+// EEGNET_LDSX_E = n (counter builds only, wrong results): drop one class of pass E's LDS accesses to
+// read its share of SQ_LDS_BANK_CONFLICT (tools/lds_probe.sh): 1 dp2 reads, 2 FIR^T windows, 3 lag
+// correlation operands, 4 dws GEMM operands, 5 dy stores, 6 e stores, 7 the in-loop LDS-DMAs
+#ifndef EEGNET_LDSX_E
+#define EEGNET_LDSX_E 0
+#endif
 template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST, class Hook>
 __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   // Adam (finalize) writes it
                                             const float* coef,    // the finalize writes it: no __restrict__
@@ -1203,7 +1218,8 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                 if (oc >= NO) break;
                 float dpq[2];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) dpq[h] = (2 * oc + h < T1) ? DP[oh * T1 + 2 * oc + h] * 0.25f : 0.f;
+                for (int h = 0; h < 2; ++h)
+                    dpq[h] = EEGNET_LDSX_E == 1 ? 0.01f * (oc + h) : (2 * oc + h < T1) ? DP[oh * T1 + 2 * oc + h] * 0.25f : 0.f;
                 float dy[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -1218,7 +1234,8 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                     sdyl += d;
                     sdyvl = fmaf(d, v, sdyvl);
                 }
-                lds_st_oct(drow + 8 * oc, oc, (floatx4){dy[0], dy[1], dy[2], dy[3]}, (floatx4){dy[4], dy[5], dy[6], dy[7]});
+                if (EEGNET_LDSX_E != 5)
+                    lds_st_oct(drow + 8 * oc, oc, (floatx4){dy[0], dy[1], dy[2], dy[3]}, (floatx4){dy[4], dy[5], dy[6], dy[7]});
             }
         }
         TRACE_PH(g, 4, 1, tph_);
@@ -1228,13 +1245,14 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
 #pragma unroll
                 for (int r = 0; r < RPW; ++r) {
                     const int o = RPW * wave + r;
-                    dma4(dp2g + (size_t)bn * ndp + o * T1 + lane, DP + o * T1);
+                    if (EEGNET_LDSX_E != 7) dma4(dp2g + (size_t)bn * ndp + o * T1 + lane, DP + o * T1);
                 }
             }
         }
         // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
         // GEMM); they land during the lag correlation / FIR^T, by the next barrier
-        if constexpr (XDMA) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
+        if constexpr (XDMA)
+            if (EEGNET_LDSX_E != 7) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 2, tph_);
         {
             float tl[K1];
@@ -1247,7 +1265,11 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                 constexpr int NT16C = (TT + 15) / 16, KQC = (NT16C + 3) / 4, NQ = RPW * KQC * NWT;
                 const int oc = fir_oct(lane);
                 float w[4 * G_::NW8];
-                lds_window<G_::NW8>(Dys + oh * RS + 8 * oc, w);
+                if (EEGNET_LDSX_E == 2) {
+#pragma unroll
+                    for (int i = 0; i < 4 * G_::NW8; ++i) w[i] = 0.001f * (lane + i);
+                } else
+                    lds_window<G_::NW8>(Dys + oh * RS + 8 * oc, w);
                 float e[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) e[i] = 0.f;
@@ -1262,8 +1284,8 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                         const int o = RPW * wave + r, a = 4 * ks + lk;
                         const bool on = a < NT16C;
                         const int ac = on ? a : 0;
-                        float av = Dys[o * RS + LP + li + 16 * ac];
-                        float bv = Ss[o * RS + G_::OFF + li + 16 * (ac + j)];
+                        float av = EEGNET_LDSX_E == 3 ? 0.01f * (li + n) : Dys[o * RS + LP + li + 16 * ac];
+                        float bv = EEGNET_LDSX_E == 3 ? 0.02f * (lk + n) : Ss[o * RS + G_::OFF + li + 16 * (ac + j)];
                         av = on ? av : 0.f;
                         bv = on ? bv : 0.f;
                         cq[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, cq[r][j], 0, 0, 0);
@@ -1273,9 +1295,10 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
 #pragma unroll
                 for (int i = 0; i < 8; ++i) e[i] = (8 * oc + i < T) ? e[i] : 0.f;
                 wave_lds_fence();                          // every dy / s read of this wave is done
-                lds_st_oct(erow + 8 * oc, oc, (floatx4){e[0], e[1], e[2], e[3]}, (floatx4){e[4], e[5], e[6], e[7]});
+                if (EEGNET_LDSX_E != 6)
+                    lds_st_oct(erow + 8 * oc, oc, (floatx4){e[0], e[1], e[2], e[3]}, (floatx4){e[4], e[5], e[6], e[7]});
                 if constexpr (PIPEE) {                     // next trial's s rows of this wave
-                    if (bn < b1) {
+                    if (bn < b1 && EEGNET_LDSX_E != 7) {
 #pragma unroll
                         for (int r = 0; r < RPW; ++r) {
                             const int o = RPW * wave + r;
@@ -1402,9 +1425,21 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
             const float* arow = Eb + (li < F2 ? li : 0) * RS + LP + 2 * lk;
             const float* brow = Xb + (c < C ? c : 0) * RS + LP + 2 * lk;
             const bool aon = li < F2, bon = c < C;
+            // the +8 halves through an offset the compiler cannot see: two plain ds_read_b64 at 8 floats
+            // apart merge into one ds_read2_b64, which banks mod 32 in 16-lane groups -- 2-way here
+            // (profiles/r5d: 2.1 M of pass E's 2.4 M conflict cycles)
+            const int o8 = 8 + opaque0();
+            const float* arow8 = arow + o8;
+            const float* brow8 = brow + o8;
             for (int kg = kg0; kg < kg1; ++kg) {
-                floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow + 16 * kg + 8);
-                floatx2 b0 = lds_ld2(brow + 16 * kg), b1 = lds_ld2(brow + 16 * kg + 8);
+                floatx2 a0, a1, b0, b1;
+                if (EEGNET_LDSX_E == 4) {
+                    a0 = (floatx2){0.01f * kg, 0.02f * li}; a1 = a0 * 2.f;
+                    b0 = (floatx2){0.03f * kg, 0.01f * lk}; b1 = b0 * 2.f;
+                } else {
+                    a0 = lds_ld2(arow + 16 * kg); a1 = lds_ld2(arow8 + 16 * kg);
+                    b0 = lds_ld2(brow + 16 * kg); b1 = lds_ld2(brow8 + 16 * kg);
+                }
                 if (!aon) { a0 = (floatx2){0.f, 0.f}; a1 = a0; }
                 if (!bon) { b0 = (floatx2){0.f, 0.f}; b1 = b0; }
                 xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b0[0], xacc, 0, 0, 0);

@@ -1421,25 +1421,23 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         constexpr int XPF = 4;
         const int cx = ct * 16 + li;
         const bool bon = cx < C;
-        // k permutation of the operands: lane lk takes t = 16 kg + 2 lk + {0, 1} and 16 kg + 8 + 2 lk +
-        // {0, 1} -- the e rows as ds_read_b64 (a 32-lane group reads 16 rows x 4 dwords, all 64 banks
-        // once; the float4 form was 2-way), x as two 8-byte loads into the same register order
-        const float* xr = x + ((size_t)b * C + (bon ? cx : 0)) * T + 2 * lk;
+        // k permutation of the operands: x goes out as one 16-byte load per k-group (lane lk: t = 16 kg +
+        // 4 lk + {0..3}), then two v_permlane16_swap exchange the middle pairs of rows lk = 0 / 1 and
+        // 2 / 3, so lane lk holds t = 16 kg + 8 (lk >> 1) + 2 (lk & 1) + {0, 1, 4, 5}.  The e rows are
+        // read in that order as two ds_read_b64: a 32-lane group (lk = 0, 1) then covers 16 rows x
+        // one whole 4-dword slot per read, all 64 banks once (RS / 4 odd); the float4 form put 16-lane
+        // groups with lk = 0 and 1 rows mixed on shared bank quads (2-way)
+        const float* xr = x + ((size_t)b * C + (bon ? cx : 0)) * T + 4 * lk;
         floatx4 xpf[XPF];
         auto xload = [&](int kgs) {
 #pragma unroll
             for (int i = 0; i < XPF; ++i) {
-                const int kg = min(kgs + i, kg1 - 1), t0 = 16 * kg + 2 * lk;
-                if ((T & 1) == 0 && t0 + 9 < T) {
-                    const floatx2 u = *reinterpret_cast<const floatx2*>(xr + 16 * kg);
-                    const floatx2 v = *reinterpret_cast<const floatx2*>(xr + 16 * kg + 8);
-                    xpf[i] = (floatx4){u[0], u[1], v[0], v[1]};
+                const int kg = min(kgs + i, kg1 - 1), t0 = 16 * kg + 4 * lk;
+                if ((T & 3) == 0 && t0 + 3 < T) {
+                    xpf[i] = *reinterpret_cast<const floatx4*>(xr + 16 * kg);
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int dt = (e & 1) + 8 * (e >> 1);
-                        xpf[i][e] = (t0 + dt < T) ? xr[16 * kg + dt] : 0.f;
-                    }
+                    for (int e = 0; e < 4; ++e) xpf[i][e] = (t0 + e < T) ? xr[16 * kg + e] : 0.f;
                 }
             }
         };
@@ -1449,14 +1447,19 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         barrier_lds();                                     // e rows complete
         TRACE_PH(g, 4, 3, tph_);
         if (gemm_on) {
-            const float* arow = Dys + li * RS + LP + 2 * lk;
+            const float* arow = Dys + li * RS + LP + 8 * (lk >> 1) + 2 * (lk & 1);
+            const float* arow4 = arow + (4 + opaque0());     // (not merged into a ds_read2_b64: pass E)
             for (int kgs = kg0; kgs < kg1; kgs += XPF) {   // (one batch at cfg5: 8 k-groups per wave)
 #pragma unroll
                 for (int i = 0; i < XPF; ++i) {
                     const int kg = kgs + i;
                     if (kg < kg1) {
-                        const floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow + 16 * kg + 8);
-                        const floatx4 b4 = bon ? xpf[i] : (floatx4){0.f, 0.f, 0.f, 0.f};
+                        const floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow4 + 16 * kg);
+                        floatx4 b4 = xpf[i];
+                        float b0 = b4[0], b1 = b4[1], b2 = b4[2], b3 = b4[3];
+                        swap16(b0, b2);                    // rows 1 / 3: t 4, 5 <-> rows 0 / 2: t 2, 3
+                        swap16(b1, b3);
+                        b4 = bon ? (floatx4){b0, b1, b2, b3} : (floatx4){0.f, 0.f, 0.f, 0.f};
                         xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b4[0], xacc, 0, 0, 0);
                         xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b4[1], xacc, 0, 0, 0);
                         xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b4[2], xacc, 0, 0, 0);
