@@ -379,9 +379,9 @@ __global__ __launch_bounds__(NTI) void k_infer_bf16(GeoI gin, const float* __res
             for (int r = 0; r < 4; ++r) {
                 const int j = ot * 16 + 4 * G + r;
                 float e = elu_f(fmaf(Co[2 * F2P + j], acc[r], Co[3 * F2P + j]));
-                e += __shfl_xor(e, 1, 64);
-                e += __shfl_xor(e, 2, 64);
-                e += __shfl_xor(e, 4, 64);
+                e += dpp<0xB1>(e);            // 8-lane sums by DPP (xor 1, xor 2, half-row mirror)
+                e += dpp<0x4E>(e);
+                e += dpp<0x141>(e);
                 if ((lane & 7) == 0 && j < F2 && t2 < g.T2) {
                     const float hv = 0.125f * e;
                     const int f = j * g.T2 + t2;

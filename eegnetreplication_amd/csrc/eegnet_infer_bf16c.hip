@@ -291,15 +291,17 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
             acc = mfma_bf16(w3f[1], tr_frag(Zi, XROWB, 32, 16 * n, lane), acc);
             // lane: r[j = ot*16 + 4G + rr][q = 16n + l15]; pool8 over the 8 lanes of q (every lane of
             // the group ends with the sums)
+            // (DPP within each 8-lane group: quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror adds the
+            // other quad -- __shfl_xor compiled to three dependent ds_bpermute round trips per row)
             float e[4];
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) e[rr] = elu_f(fmaf(s3r[rr], acc[rr], b3r[rr]));
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) e[rr] += __shfl_xor(e[rr], 1, 64);
+            for (int rr = 0; rr < 4; ++rr) e[rr] += dpp<0xB1>(e[rr]);
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) e[rr] += __shfl_xor(e[rr], 2, 64);
+            for (int rr = 0; rr < 4; ++rr) e[rr] += dpp<0x4E>(e[rr]);
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) e[rr] += __shfl_xor(e[rr], 4, 64);
+            for (int rr = 0; rr < 4; ++rr) e[rr] += dpp<0x141>(e[rr]);
             const float hv = 0.125f * (prr == 0 ? e[0] : prr == 1 ? e[1] : prr == 2 ? e[2] : e[3]);
             lp0 = fmaf(wfl[m][0], hv, lp0);
             lp1 = fmaf(wfl[m][1], hv, lp1);

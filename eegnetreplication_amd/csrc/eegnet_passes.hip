@@ -726,9 +726,9 @@ __global__ __launch_bounds__(NTH) void k_infer(Geo g, const float* __restrict__ 
         for (int m = 0; m < MAXT1Q; ++m) {
             const int t = lane + 64 * m;
             float e = (row_on && t < 8 * T2) ? elu_f(fmaf(s3, r[m], b3)) : 0.f;
-            e += __shfl_xor(e, 1, 64);
-            e += __shfl_xor(e, 2, 64);
-            e += __shfl_xor(e, 4, 64);
+            e += dpp<0xB1>(e);                 // 8-lane sums by DPP (xor 1, xor 2, half-row mirror)
+            e += dpp<0x4E>(e);
+            e += dpp<0x141>(e);
             if (row_on && (t & 7) == 0 && t < 8 * T2) Hs[o * T2 + (t >> 3)] = e * 0.125f;
         }
         __syncthreads();
