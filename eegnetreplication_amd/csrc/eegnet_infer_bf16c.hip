@@ -12,9 +12,14 @@
 //   halo, 16 KB, two buffers) and s rows (12 KB) are all the full-rate data in LDS, and the pooled
 //   rows a (bf16, 18 KB) accumulate over the chunks.  74 KB per workgroup: two workgroups (16 waves)
 //   per CU, on different trials and out of phase.
-// * x arrives by LDS-DMA (global_load_lds_dwordx4) straight into the XOR-swizzled transposed-read
-//   image -- the swizzle is applied to the per-lane SOURCE address, the 16-byte units of a wave land
-//   contiguously -- two chunks ahead, with no prefetch registers (<= 128 VGPRs for 4 waves / SIMD).
+// * x arrives by LDS-DMA (global_load_lds_dwordx4) straight into the swizzled transposed-read image
+//   -- the swizzle is applied to the per-lane SOURCE address, the 16-byte units of a wave land
+//   contiguously -- one chunk ahead, with no prefetch registers (<= 128 VGPRs for 4 waves / SIMD).
+// * Round 5: ONE workgroup barrier per chunk.  The s rows are double-buffered, so chunk j's spatial
+//   GEMM and chunk j - 1's FIR run in the same barrier interval (19 -> 12 barriers per trial); the
+//   LDS for the second s buffer comes from the x images' unused quarter (rows of 192 bytes, the 96
+//   samples of a chunk, instead of 256) and from the w1 table (the FIR taps are read from global
+//   memory once, into registers).
 // * FIR on the matrix cores with a full MFMA per chunk: the 16 columns are (row r of a temporal
 //   group, 16-sample tile) -- the D = 4 rows of a group share the banded Toeplitz A operand of the
 //   group's taps -- so a 64-sample chunk still fills all 16 columns.
@@ -32,22 +37,24 @@ constexpr int C = 64, T = 512, F1 = 16, D = 4, F2 = 64, K1 = 32, T1 = 128, T2 = 
 constexpr int TC = 64;                       // output samples per chunk: D rows x TC/16 tiles = 16 columns
 constexpr int NCH = T / TC;                  // chunks per trial
 constexpr int NTS = 6;                       // spatial 16-sample tiles per chunk (64j - 16 .. 64j + 80)
-constexpr int XROWB = 256;                   // x image row (bytes): 128 bf16, 96 used; swizzle needs 128
-constexpr int XIMG = C * XROWB;              // 16 KB per chunk buffer
+constexpr int XROWB = 192;                   // x image row (bytes): the chunk's 96 samples
+constexpr int XIMG = C * XROWB;              // 12 KB per chunk buffer
+constexpr int ZROWB = 256;                   // z image row (bytes): 128 pooled samples (block-2 tail)
 constexpr int SROW = 120;                    // s row stride (bf16): 112 read, 60 dwords = 4 mod 8
 constexpr int AROW = 144;                    // a row (bf16): [8 zeros | 128 pooled | 8 zeros]
 constexpr int W2R = 48;                      // depthwise taps, bf16, [16 zeros | 16 taps | 16 zeros]
 constexpr int NT = 512;                      // threads: 8 waves
 constexpr int NW = NT / 64;
-// LDS carve (bytes)
+// LDS carve (bytes): x images 0 / 1, s rows 0 / 1 (the z image of the tail over both), a rows, tables
+constexpr int SIMG = F2 * SROW * 2;
 constexpr int OFF_X0 = 0, OFF_X1 = XIMG, OFF_S = 2 * XIMG;
-constexpr int OFF_A = OFF_S + F2 * SROW * 2;
-constexpr int OFF_W1 = OFF_A + F2 * AROW * 2;
-constexpr int OFF_W2 = OFF_W1 + F1 * K1 * 4;
+constexpr int OFF_A = OFF_S + 2 * SIMG;
+constexpr int OFF_W2 = OFF_A + F2 * AROW * 2;
 constexpr int OFF_CO = OFF_W2 + F2 * W2R * 2;
 constexpr int OFF_LG = OFF_CO + 4 * F2 * 4;
 constexpr int LDS = OFF_LG + NW * NCLS * 4;
 static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+static_assert(F2 * ZROWB <= 2 * SIMG, "the z image fits over the two s buffers");
 static_assert(F2 % 16 == 0 && 16 % D == 0 && TC == 16 * (16 / D), "FIR columns = rows of a group x tiles");
 
 }  // namespace c5
@@ -63,23 +70,41 @@ __device__ __forceinline__ void dma16c(const void* gsrc, const void* ldst) {
 }
 
 // chunk j of trial xb (bf16 [C][T]) into an x image: samples 64j - 16 .. 64j + 79 of every channel row,
-// 16-byte units u = 0..11 of the row; physical unit u' of row r holds unit u' ^ 2h(r) (trimg_off's 8-byte
-// chunk swizzle ch ^ 4h, on unit pairs).  Units outside the trial read zeros ('same' padding).  Each
-// wave issues 2 wave-instructions (4 rows each).
+// 16-byte units u = 0..11 of the row.  Row r of the image is 192 bytes at 192 r; its 32-byte groups are
+// swizzled g -> g ^ sig(r), sig(r) = bit 3 of r (x_img_off), so physical unit u' holds unit u' ^ 2 sig(r).
+// One wave-instruction writes 4 rows (48 lanes x 16 bytes, contiguous); units outside the trial read
+// zeros ('same' padding).  Each wave issues 2 wave-instructions.
 __device__ __forceinline__ void x_chunk_dma(const uint16_t* __restrict__ xb, int j, char* img, int wave, int lane) {
     using namespace c5;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r0 = 4 * (wave + NW * i);
-        const int r = r0 + (lane >> 4), up = lane & 15;
-        const int h = (r & 3) | ((r >> 1) & 4);
-        const int u = up ^ (2 * h);
-        if (u < 12) {
+        const int rr = lane / 12, up = lane - 12 * rr;
+        const int r = r0 + rr;
+        const int u = up ^ (2 * ((r >> 3) & 1));
+        if (lane < 48) {
             const int s0 = TC * j - 16 + 8 * u;
             const void* src = (s0 >= 0 && s0 < T) ? (const void*)(xb + (size_t)r * T + s0) : (const void*)g_zero16;
             dma16c(src, img + r0 * XROWB);
         }
     }
+}
+
+// byte offset of 8-byte chunk `ch` of row r in the x image.  A ds_read_b64_tr_b16 half-wave reads
+// rows k0 + q and k0 + 8 + q (q = 0..3), 32 bytes each: 192-byte rows put row q's bytes at bank
+// offset 48 q mod 64 dwords (0, 48, 32, 16), and the group swizzle moves rows 8..11 by one 32-byte
+// group (8 dwords): the 8 rows cover the 64 banks once
+__device__ __forceinline__ int x_img_off(int r, int ch) {
+    return r * c5::XROWB + 8 * (ch ^ (4 * ((r >> 3) & 1)));
+}
+__device__ __forceinline__ bf16x8 tr_frag_x(const char* img, int k0, int n0, int lane) {
+    const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int r = k0 + 8 * G + q;
+    const int ch = (n0 >> 2) + p;
+    const shortx4 lo = lds_tr16(img + x_img_off(r, ch));
+    const shortx4 hi = lds_tr16(img + x_img_off(r + 4, ch));
+    const shortx8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
 }
 
 template <int N>
@@ -97,10 +122,9 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
                                                                float* __restrict__ logits) {
     using namespace c5;
     extern __shared__ __attribute__((aligned(16))) char smc[];
-    char* const Si = smc + OFF_S;                       // s rows (bf16) of the current chunk
     char* const Ai = smc + OFF_A;                       // pooled rows a (bf16), whole trial
-    char* const Zi = smc + OFF_X1;                      // z image (bf16, swizzled): x buffer 1 after chunk 7
-    float* const W1t = reinterpret_cast<float*>(smc + OFF_W1);
+    char* const Zi = smc + OFF_S;                       // z image (bf16, swizzled, 256-byte rows): over the
+                                                        // two s buffers, between trials
     uint16_t* const W2p = reinterpret_cast<uint16_t*>(smc + OFF_W2);
     float* const Co = reinterpret_cast<float*>(smc + OFF_CO);   // [4][F2]: al, be, s3, b3
     float* const Lg = reinterpret_cast<float*>(smc + OFF_LG);   // [NW][4] logit partials
@@ -109,12 +133,10 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
     const int G = lane >> 4, l15 = lane & 15;
     const int B = g.B;
 
-    // ---- prologue: next x DMA first (the tables below overlap it), then tables and zero pads ----
+    // ---- prologue: the first trial's chunk 0 DMA first (the tables below overlap it), then tables
+    // and zero pads ----
     int b = blockIdx.x;
-    if (b < B) {
-        x_chunk_dma(x + (size_t)b * C * T, 0, smc + OFF_X0, wave, lane);
-        x_chunk_dma(x + (size_t)b * C * T, 1, smc + OFF_X1, wave, lane);
-    }
+    if (b < B) x_chunk_dma(x + (size_t)b * C * T, 0, smc + OFF_X0, wave, lane);
     if (tid < F2) {
         const int o = tid, gg = o / D;
         const float* rm1 = bn;             const float* rv1 = bn + F1;
@@ -131,13 +153,23 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
         Co[2 * F2 + o] = s3;
         Co[3 * F2 + o] = prm[g.o_b3 + o] - rm3[o] * s3;
     }
-    for (int i = tid; i < F1 * K1; i += NT) W1t[i] = prm[g.o_w1 + i];
-    for (int i = tid; i < F2 * W2R; i += NT) {
-        const int o = i / W2R, k = i - o * W2R - 16;
-        W2p[i] = __builtin_bit_cast(uint16_t, (__bf16)((k >= 0 && k < K2) ? prm[g.o_w2 + o * K2 + k] : 0.f));
+    {
+        constexpr int NW2 = (F2 * W2R + NT - 1) / NT;
+        float w2v[NW2];
+#pragma unroll
+        for (int u = 0; u < NW2; ++u) {
+            const int i = min(tid + NT * u, F2 * W2R - 1), o = i / W2R, k = i - o * W2R - 16;
+            w2v[u] = prm[g.o_w2 + o * K2 + min(max(k, 0), K2 - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < NW2; ++u) {
+            const int i = tid + NT * u, o = i / W2R, k = i - o * W2R - 16;
+            if (i < F2 * W2R) W2p[i] = __builtin_bit_cast(uint16_t, (__bf16)((k >= 0 && k < K2) ? w2v[u] : 0.f));
+        }
     }
-    // s rows: positions 96..111 meet only zero taps but must be finite; a rows: 'same' pads of the dw16
-    for (int i = tid; i < F2 * SROW / 2; i += NT) reinterpret_cast<uint32_t*>(Si)[i] = 0u;
+    // s rows: positions 96..111 meet only zero taps but must be finite (the z image of a previous
+    // trial leaves finite values there); a rows: 'same' pads of the dw16
+    for (int i = tid; i < 2 * F2 * SROW / 2; i += NT) reinterpret_cast<uint32_t*>(smc + OFF_S)[i] = 0u;
     for (int i = tid; i < F2 * AROW / 2; i += NT) reinterpret_cast<uint32_t*>(Ai)[i] = 0u;
 
     // spatial GEMM: this wave's o-tile (ws^T B operand, K = c, both K-steps in registers) and t-tiles
@@ -155,45 +187,46 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj)
             w3f[ks][jj] = (__bf16)prm[g.o_W3 + (ot * 16 + l15) * F2 + ks * 32 + 8 * G + jj];
-    __syncthreads();                                   // tables (not the DMA: asm, waited per chunk)
-
     // FIR: this wave's two temporal groups gi = 2 wave + {0, 1}; banded Toeplitz A operand of each
     // group's taps, A[i][j] = w1[g][j - i - 1] over K = 64 (two K-steps), held for the whole kernel;
     // this lane's FIR column is (row r = l15 >> 2 of the group, tile l15 & 3)
+    // (unconditional loads at clamped taps, masked after: a guarded load is a branch and a full wait
+    // each -- 32 serialised L2 round trips per workgroup)
     bf16x8 af[2][2];
+    {
+        float wv[2][2][8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                    const int k = 32 * s + 8 * G + jj - l15 - 1;
+                    wv[q][s][jj] = prm[g.o_w1 + (2 * wave + q) * K1 + min(max(k, 0), K1 - 1)];
+                }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                    const int k = 32 * s + 8 * G + jj - l15 - 1;
+                    af[q][s][jj] = (__bf16)((k >= 0 && k < K1) ? wv[q][s][jj] : 0.f);
+                }
+    }
+    __syncthreads();                                   // tables (not the DMA: asm, waited per chunk)
     float al2[2], be2[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-        const int gg = 2 * wave + q;
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-                const int k = 32 * s + 8 * G + jj - l15 - 1;
-                af[q][s][jj] = (__bf16)((k >= 0 && k < K1) ? W1t[gg * K1 + k] : 0.f);
-            }
-        const int o = D * gg + (l15 >> 2);
+        const int o = D * (2 * wave + q) + (l15 >> 2);
         al2[q] = Co[o] * 1.4426950408889634f;              // ELU in log2 units (k_infer_bf16)
         be2[q] = Co[F2 + o] * 1.4426950408889634f;
     }
-    // pointwise epilogue constants of this lane's 4 output rows j = ot*16 + 4G + rr
-    float s3r[4], b3r[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        s3r[rr] = Co[2 * F2 + ot * 16 + 4 * G + rr];
-        b3r[rr] = Co[3 * F2 + ot * 16 + 4 * G + rr];
-    }
-    // classifier weights this lane multiplies, held for the whole kernel: after pool8 every lane of an
-    // 8-lane group holds the group's 4 pooled values (rows rr); lane p = l15 & 7 takes row rr = p >> 1
-    // and classes 2 (p & 1), 2 (p & 1) + 1, for each of its wave's 4 pointwise tiles (8 weights)
+    // classifier weights this lane multiplies: after pool8 every lane of an 8-lane group holds the
+    // group's 4 pooled values (rows rr); lane p = l15 & 7 takes row rr = p >> 1 and classes 2 (p & 1),
+    // 2 (p & 1) + 1, for each of its wave's 4 pointwise tiles (8 weights).  Loaded per trial at the
+    // tail, like the BN3 constants: registers held across the chunk loop serialised its phases
     const int prr = (l15 & 7) >> 1, pc0 = 2 * (l15 & 1);
-    float wfl[4][2];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int f = (ot * 16 + 4 * G + prr) * T2 + 2 * (tt0 + 2 * m) + (l15 >> 3);
-        wfl[m][0] = prm[g.o_Wfc + pc0 * NF + f];
-        wfl[m][1] = prm[g.o_Wfc + (pc0 + 1) * NF + f];
-    }
 #ifdef EEGNET_TRACE
     // traced build (tools/trace_bf16.py): thread 0's shader cycles per phase, summed over the trials
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_ = clock64();
@@ -202,62 +235,113 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
 #define PH_(k) do {} while (0)
 #endif
 
+    // FIR (banded Toeplitz MFMA), folded BN, ELU, pool4 of chunk jf from s buffer Sf -> a rows
+    // (reads, then MFMAs: issuing the reads before the spatial GEMM's stores instead spilled 10 VGPRs)
+    constexpr int NQ = (EEGNET_KX == 2 || EEGNET_KX == 4) ? 0 : 2;
+    bf16x8 fw[2][2];
+    auto fir_load = [&](const char* Sf) {                  // both groups' s windows
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int o = D * (2 * wave + q) + (l15 >> 2), tile = l15 & 3;
+            const char* srw = Sf + o * (2 * SROW) + 2 * (16 * tile + 8 * G);
+            fw[q][0] = *reinterpret_cast<const bf16x8*>(srw);
+            fw[q][1] = *reinterpret_cast<const bf16x8*>(srw + 64);
+        }
+    };
+    auto fir_chunk = [&](int jf) {
+        floatx4 facc[2];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
+            facc[q] = mfma_bf16(af[q][0], fw[q][0], z4);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) facc[q] = mfma_bf16(af[q][1], fw[q][1], facc[q]);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int gg = 2 * wave + q;
+            const int o = D * gg + (l15 >> 2), tile = l15 & 3;
+            const floatx4 acc = facc[q];
+            // lane: v[o][t = 64 jf + 16 tile + 4G + r]; pooled sample 16 jf + 4 tile + G
+            float pp = 0.f, pn = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float y = fmaf(al2[q], acc[r], be2[q]);
+                pp += fmaxf(y, 0.f);
+                pn += __builtin_amdgcn_exp2f(fminf(y, 0.f));
+            }
+            const float a = fmaf(0.25f * 0.6931471805599453f, pp, 0.25f * pn - 1.f);
+            reinterpret_cast<__bf16*>(Ai)[o * AROW + 8 + 16 * jf + 4 * tile + G] = (__bf16)a;
+        }
+    };
+
     for (; b < B; b += gridDim.x) {
         const bool more = b + (int)gridDim.x < B;
         const uint16_t* xn = x + (size_t)(b + gridDim.x) * C * T;
+        // Per chunk j, ONE barrier: x chunk j landed (its DMA, issued at the top of chunk j - 1, is
+        // the only one in flight), s buffer j & 1 free (chunk j - 2's FIR finished before the previous
+        // barrier), s buffer (j - 1) & 1 complete (chunk j - 1's spatial GEMM, idem), x buffer
+        // (j + 1) & 1 free (read by chunk j - 1's spatial GEMM).  Then: the next chunk's DMA, this
+        // chunk's spatial GEMM and the previous chunk's FIR.
 #pragma unroll 1
         for (int j = 0; j < NCH; ++j) {
             char* const Xi = smc + ((j & 1) ? OFF_X1 : OFF_X0);
-            // x chunk j landed (every wave's DMAs; each wave has 2 newer ones in flight unless none was
-            // issued after: chunk 7 of the last trial); the previous chunk's FIR is done with Si
-            if (j < NCH - 1 || more) barrier_vm_c<2>();
-            else barrier_vm_c<0>();
+            char* const Si = smc + OFF_S + (j & 1) * SIMG;
+            barrier_vm_c<0>();
             PH_(0);
-            // ---- 1. spatial GEMM s^T[t][o] (16 t x 16 o tiles, A = x^T by transposed reads) ----
+            if (EEGNET_KX == 5) {
+            } else if (j + 1 < NCH) x_chunk_dma(x + (size_t)b * C * T, j + 1, smc + (((j + 1) & 1) ? OFF_X1 : OFF_X0), wave, lane);
+            else if (more) x_chunk_dma(xn, 0, smc + OFF_X0, wave, lane);      // next trial's chunk 0
+            // ---- spatial GEMM s^T[t][o] (16 t x 16 o tiles, A = x^T by transposed reads): every
+            // tile's transposed reads first, then the MFMAs, then the stores (one tile at a time, the
+            // compiler reused the fragment registers and serialised read -> MFMA -> store per tile) ----
+            constexpr int NSP = (EEGNET_KX == 1 || EEGNET_KX == 4) ? 0 : 3;
+            bf16x8 sa[3][2];
 #pragma unroll
-            for (int m = 0; m < ((EEGNET_KX == 1 || EEGNET_KX == 4) ? 0 : 3); ++m) {
-                const int n = tt0 + 2 * m;
+            for (int m = 0; m < NSP; ++m) {
+                sa[m][0] = tr_frag_x(Xi, 0, 16 * (tt0 + 2 * m), lane);
+                sa[m][1] = tr_frag_x(Xi, 32, 16 * (tt0 + 2 * m), lane);
+            }
+            floatx4 sacc[3];
+#pragma unroll
+            for (int m = 0; m < NSP; ++m) {
                 const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
-                const bf16x8 a0 = tr_frag(Xi, XROWB, 0, 16 * n, lane), a1 = tr_frag(Xi, XROWB, 32, 16 * n, lane);
-                floatx4 acc = mfma_bf16(a0, wsf[0], z4);
-                acc = mfma_bf16(a1, wsf[1], acc);
+                sacc[m] = mfma_bf16(sa[m][0], wsf[0], z4);
+            }
+#pragma unroll
+            for (int m = 0; m < NSP; ++m) sacc[m] = mfma_bf16(sa[m][1], wsf[1], sacc[m]);
+#pragma unroll
+            for (int m = 0; m < NSP; ++m) {
                 uintx2 pk;
-                pk[0] = pack_bf16x2(acc[0], acc[1]);
-                pk[1] = pack_bf16x2(acc[2], acc[3]);
-                *reinterpret_cast<uintx2*>(Si + (ot * 16 + l15) * (2 * SROW) + 2 * (16 * n + 4 * G)) = pk;
+                pk[0] = pack_bf16x2(sacc[m][0], sacc[m][1]);
+                pk[1] = pack_bf16x2(sacc[m][2], sacc[m][3]);
+                *reinterpret_cast<uintx2*>(Si + (ot * 16 + l15) * (2 * SROW) + 2 * (16 * (tt0 + 2 * m) + 4 * G)) = pk;
             }
             PH_(1);
-            barrier_lds_c();                               // s rows complete; x buffer consumed
-            PH_(2);
-            if (EEGNET_KX == 5) {
-            } else if (j + 2 < NCH) x_chunk_dma(x + (size_t)b * C * T, j + 2, Xi, wave, lane);
-            else if (j == NCH - 2 && more) x_chunk_dma(xn, 0, Xi, wave, lane);   // next trial's chunk 0
-            // ---- 2. FIR (banded Toeplitz MFMA), folded BN, ELU, pool4 -> a rows ----
-#pragma unroll
-            for (int q = 0; q < ((EEGNET_KX == 2 || EEGNET_KX == 4) ? 0 : 2); ++q) {
-                const int gg = 2 * wave + q;
-                const int o = D * gg + (l15 >> 2), tile = l15 & 3;
-                const char* srw = Si + o * (2 * SROW) + 2 * (16 * tile + 8 * G);
-                floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-                acc = mfma_bf16(af[q][0], *reinterpret_cast<const bf16x8*>(srw), acc);
-                acc = mfma_bf16(af[q][1], *reinterpret_cast<const bf16x8*>(srw + 64), acc);
-                // lane: v[o][t = 64j + 16 tile + 4G + r]; pooled sample 16j + 4 tile + G
-                float pp = 0.f, pn = 0.f;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float y = fmaf(al2[q], acc[r], be2[q]);
-                    pp += fmaxf(y, 0.f);
-                    pn += __builtin_amdgcn_exp2f(fminf(y, 0.f));
-                }
-                const float a = fmaf(0.25f * 0.6931471805599453f, pp, 0.25f * pn - 1.f);
-                reinterpret_cast<__bf16*>(Ai)[o * AROW + 8 + 16 * j + 4 * tile + G] = (__bf16)a;
+            if (j > 0) {                                   // the previous chunk's FIR
+                fir_load(smc + OFF_S + ((j - 1) & 1) * SIMG);
+                fir_chunk(j - 1);
             }
             PH_(3);
         }
-        barrier_lds_c();                                   // a rows complete (the 8 chunks); x buffer 1 free
+        barrier_lds_c();                                   // chunk 7's s rows complete
+        PH_(2);
+        fir_load(smc + OFF_S + ((NCH - 1) & 1) * SIMG);
+        fir_chunk(NCH - 1);
+        PH_(3);
+        barrier_lds_c();                                   // a rows complete; the s buffers are free
         PH_(4);
 
-        // ---- 3. depthwise 1x16 (pad 7 | 8) on the matrix cores -> z image (x buffer 1) ----
+        // the tail's per-lane constants (L2-resident classifier weights, BN3 constants from LDS): issued
+        // here, used after the depthwise
+        float wfl[4][2];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int f = (ot * 16 + 4 * G + prr) * T2 + 2 * (tt0 + 2 * m) + (l15 >> 3);
+            wfl[m][0] = prm[g.o_Wfc + pc0 * NF + f];
+            wfl[m][1] = prm[g.o_Wfc + (pc0 + 1) * NF + f];
+        }
+        // ---- depthwise 1x16 (pad 7 | 8) on the matrix cores -> z image (over the s buffers) ----
         // z[o][16n + i] = sum_j A[i][j] W_n[j], A[i][j] = w2[o][j - i - 1], W_n[j] = a[o][16n + j - 8]
 #pragma unroll 4
         for (int rr = 0; rr < ((EEGNET_KX == 3 || EEGNET_KX == 4) ? 0 : F2 / NW); ++rr) {
@@ -274,25 +358,31 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
                 uintx2 pk;
                 pk[0] = pack_bf16x2(acc[0], acc[1]);
                 pk[1] = pack_bf16x2(acc[2], acc[3]);
-                *reinterpret_cast<uintx2*>(Zi + trimg_off(o, 4 * l15 + G, XROWB)) = pk;
+                *reinterpret_cast<uintx2*>(Zi + trimg_off(o, 4 * l15 + G, ZROWB)) = pk;
             }
         }
         PH_(5);
         barrier_lds_c();
         PH_(4);
 
-        // ---- 4. pointwise MFMA (A = W3, B = z by transposed reads), BN3, ELU, pool8, classifier ----
+        // ---- pointwise MFMA (A = W3, B = z by transposed reads), BN3, ELU, pool8, classifier ----
+        float s3r[4], b3r[4];                              // this lane's 4 output rows j = ot*16 + 4G + rr
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            s3r[rr] = Co[2 * F2 + ot * 16 + 4 * G + rr];
+            b3r[rr] = Co[3 * F2 + ot * 16 + 4 * G + rr];
+        }
         float lp0 = 0.f, lp1 = 0.f;                       // classes pc0, pc0 + 1 of this lane's row prr
 #pragma unroll
         for (int m = 0; m < ((EEGNET_KX == 3 || EEGNET_KX == 4) ? 0 : 4); ++m) {
             const int n = tt0 + 2 * m;
             floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-            acc = mfma_bf16(w3f[0], tr_frag(Zi, XROWB, 0, 16 * n, lane), acc);
-            acc = mfma_bf16(w3f[1], tr_frag(Zi, XROWB, 32, 16 * n, lane), acc);
+            acc = mfma_bf16(w3f[0], tr_frag(Zi, ZROWB, 0, 16 * n, lane), acc);
+            acc = mfma_bf16(w3f[1], tr_frag(Zi, ZROWB, 32, 16 * n, lane), acc);
             // lane: r[j = ot*16 + 4G + rr][q = 16n + l15]; pool8 over the 8 lanes of q (every lane of
-            // the group ends with the sums)
-            // (DPP within each 8-lane group: quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror adds the
-            // other quad -- __shfl_xor compiled to three dependent ds_bpermute round trips per row)
+            // the group ends with the sums).  DPP within each 8-lane group: quad_perm [1,0,3,2],
+            // [2,3,0,1], then row_half_mirror adds the other quad (__shfl_xor compiled to three
+            // dependent ds_bpermute round trips per row)
             float e[4];
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) e[rr] = elu_f(fmaf(s3r[rr], acc[rr], b3r[rr]));
@@ -323,7 +413,6 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
             for (int w = 0; w < NW; ++w) a += Lg[w * NCLS + tid];
             logits[(size_t)b * NCLS + tid] = a;
         }
-        if (more && EEGNET_KX != 5) x_chunk_dma(xn, 1, smc + OFF_X1, wave, lane);  // next trial's chunk 1
         PH_(7);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -1414,38 +1414,57 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
             if constexpr (VPF) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
         }
         TRACE_PH(g, 4, 5, tph_);
-        // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores; lane lk holds 4 consecutive t of
-        // each 16-t group as a float4 (the k order inside a group is permuted identically in A and B)
+        // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores (16 e rows x 16 x rows of this wave's
+        // c-tile; the k order inside the wave's t range is permuted identically in A and B)
         if (gemm_on) {
-            // operands by ds_read_b64: lane lk takes t = 16 kg + 2 lk + {0, 1} and 16 kg + 8 + 2 lk +
-            // {0, 1} (the same permutation of k in A and B).  A 32-lane group then reads 16 rows x 4
-            // dwords = all 64 banks once (RS / 4 odd); the float4 form (ds_read_b128, 16-lane groups
-            // with lk = 0 and 1 rows mixed) put 7 of its 16 lanes on a busy bank quad: 2-way
             const int c = ct * 16 + li;
-            const float* arow = Eb + (li < F2 ? li : 0) * RS + LP + 2 * lk;
-            const float* brow = Xb + (c < C ? c : 0) * RS + LP + 2 * lk;
             const bool aon = li < F2, bon = c < C;
-            // the +8 halves through an offset the compiler cannot see: two plain ds_read_b64 at 8 floats
-            // apart merge into one ds_read2_b64, which banks mod 32 in 16-lane groups -- 2-way here
-            // (profiles/r5d: 2.1 M of pass E's 2.4 M conflict cycles)
-            const int o8 = 8 + opaque0();
-            const float* arow8 = arow + o8;
-            const float* brow8 = brow + o8;
-            for (int kg = kg0; kg < kg1; ++kg) {
-                floatx2 a0, a1, b0, b1;
-                if (EEGNET_LDSX_E == 4) {
-                    a0 = (floatx2){0.01f * kg, 0.02f * li}; a1 = a0 * 2.f;
-                    b0 = (floatx2){0.03f * kg, 0.01f * lk}; b1 = b0 * 2.f;
-                } else {
-                    a0 = lds_ld2(arow + 16 * kg); a1 = lds_ld2(arow8 + 16 * kg);
-                    b0 = lds_ld2(brow + 16 * kg); b1 = lds_ld2(brow8 + 16 * kg);
+            if constexpr (TT != 0 && TT % 128 == 0) {
+                // k-group kg of a 128-sample block: lane lk takes the float4 at t = 128 (kg >> 3) +
+                // 8 (kg & 7) + 64 (lk & 1) + 4 (lk >> 1), one ds_read_b128 per operand.  The 16-lane
+                // groups of ds_read_b128 ({0-3, 12-15, 20-27}, ...) pair lk = 0 with 1 and 2 with 3, whose
+                // offsets now agree mod 64 floats (one bank row): a group is 16 distinct rows li, each on
+                // its own 4-bank slot (RS / 4 odd) -- conflict-free at one instruction per operand (the
+                // plain t = 16 kg + 4 lk order was 2-way; two ds_read_b64 per operand are conflict-free
+                // but cost more issue than the conflicts did)
+                const int lo = 64 * (lk & 1) + 4 * (lk >> 1);
+                const float* arow = Eb + (aon ? li : 0) * RS + LP + lo;
+                const float* brow = Xb + (bon ? c : 0) * RS + LP + lo;
+                for (int kg = kg0; kg < kg1; ++kg) {
+                    const int to = 128 * (kg >> 3) + 8 * (kg & 7);
+                    floatx4 a4, b4;
+                    if (EEGNET_LDSX_E == 4) {
+                        a4 = (floatx4){0.01f * kg, 0.02f * li, 0.f, 1.f};
+                        b4 = (floatx4){0.03f * kg, 0.01f * lk, 1.f, 0.f};
+                    } else {
+                        a4 = lds_ld4(arow + to);
+                        b4 = lds_ld4(brow + to);
+                    }
+                    if (!aon) a4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+                    if (!bon) b4 = (floatx4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], xacc, 0, 0, 0);
                 }
-                if (!aon) { a0 = (floatx2){0.f, 0.f}; a1 = a0; }
-                if (!bon) { b0 = (floatx2){0.f, 0.f}; b1 = b0; }
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b0[0], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b0[1], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b1[0], xacc, 0, 0, 0);
-                xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b1[1], xacc, 0, 0, 0);
+            } else {
+                // operands by ds_read_b64: lane lk takes t = 16 kg + 2 lk + {0, 1} and 16 kg + 8 + 2 lk +
+                // {0, 1}.  A 32-lane group then reads 16 rows x 4 dwords = all 64 banks once (RS / 4 odd).
+                // The +8 halves go through an offset the compiler cannot see: two plain ds_read_b64 8
+                // floats apart merge into one ds_read2_b64, which banks mod 32 in 16-lane groups (2-way)
+                const float* arow = Eb + (aon ? li : 0) * RS + LP + 2 * lk;
+                const float* brow = Xb + (bon ? c : 0) * RS + LP + 2 * lk;
+                const int o8 = 8 + opaque0();
+                const float* arow8 = arow + o8;
+                const float* brow8 = brow + o8;
+                for (int kg = kg0; kg < kg1; ++kg) {
+                    floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow8 + 16 * kg);
+                    floatx2 b0 = lds_ld2(brow + 16 * kg), b1 = lds_ld2(brow8 + 16 * kg);
+                    if (!aon) { a0 = (floatx2){0.f, 0.f}; a1 = a0; }
+                    if (!bon) { b0 = (floatx2){0.f, 0.f}; b1 = b0; }
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b0[0], xacc, 0, 0, 0);
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b0[1], xacc, 0, 0, 0);
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b1[0], xacc, 0, 0, 0);
+                    xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b1[1], xacc, 0, 0, 0);
+                }
             }
         }
         if (bn < b1) {

@@ -1421,23 +1421,27 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         constexpr int XPF = 4;
         const int cx = ct * 16 + li;
         const bool bon = cx < C;
-        // k permutation of the operands: x goes out as one 16-byte load per k-group (lane lk: t = 16 kg +
-        // 4 lk + {0..3}), then two v_permlane16_swap exchange the middle pairs of rows lk = 0 / 1 and
-        // 2 / 3, so lane lk holds t = 16 kg + 8 (lk >> 1) + 2 (lk & 1) + {0, 1, 4, 5}.  The e rows are
-        // read in that order as two ds_read_b64: a 32-lane group (lk = 0, 1) then covers 16 rows x
-        // one whole 4-dword slot per read, all 64 banks once (RS / 4 odd); the float4 form put 16-lane
-        // groups with lk = 0 and 1 rows mixed on shared bank quads (2-way)
-        const float* xr = x + ((size_t)b * C + (bon ? cx : 0)) * T + 4 * lk;
+        // k permutation of the operands (the same in A and B).  cfg5 (SPEC, T = 512): k-group kg of a
+        // 128-sample block gives lane lk the float4 at t = 128 (kg >> 3) + 8 (kg & 7) + 64 (lk & 1) +
+        // 4 (lk >> 1): x is one 16-byte global load, the e rows one ds_read_b128 whose 16-lane groups
+        // (lk = 0 with 1, 2 with 3) read 16 distinct rows at offsets equal mod 64 floats -- conflict-free
+        // (pass E's narrow GEMM, eegnet_stream.hip).  Other shapes: x as a 16-byte load of t = 16 kg +
+        // 4 lk + {0..3}, two v_permlane16_swap exchange the middle pairs of rows lk = 0 / 1 and 2 / 3,
+        // and the e rows are read in that order as two ds_read_b64 (a 32-lane group covers 16 rows x
+        // one 4-dword slot per read)
+        const int lo = SPEC ? 64 * (lk & 1) + 4 * (lk >> 1) : 4 * lk;
+        auto tof = [&](int kg) { return SPEC ? 128 * (kg >> 3) + 8 * (kg & 7) : 16 * kg; };
+        const float* xr = x + ((size_t)b * C + (bon ? cx : 0)) * T + lo;
         floatx4 xpf[XPF];
         auto xload = [&](int kgs) {
 #pragma unroll
             for (int i = 0; i < XPF; ++i) {
-                const int kg = min(kgs + i, kg1 - 1), t0 = 16 * kg + 4 * lk;
+                const int kg = min(kgs + i, kg1 - 1), t0 = tof(kg) + lo;
                 if ((T & 3) == 0 && t0 + 3 < T) {
-                    xpf[i] = *reinterpret_cast<const floatx4*>(xr + 16 * kg);
+                    xpf[i] = *reinterpret_cast<const floatx4*>(xr + tof(kg));
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) xpf[i][e] = (t0 + e < T) ? xr[16 * kg + e] : 0.f;
+                    for (int e = 0; e < 4; ++e) xpf[i][e] = (t0 + e < T) ? xr[tof(kg) + e] : 0.f;
                 }
             }
         };
@@ -1447,23 +1451,30 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         barrier_lds();                                     // e rows complete
         TRACE_PH(g, 4, 3, tph_);
         if (gemm_on) {
-            const float* arow = Dys + li * RS + LP + 8 * (lk >> 1) + 2 * (lk & 1);
-            const float* arow4 = arow + (4 + opaque0());     // (not merged into a ds_read2_b64: pass E)
+            const float* arow = Dys + li * RS + LP + (SPEC ? lo : 8 * (lk >> 1) + 2 * (lk & 1));
+            const float* arow4 = arow + (4 + opaque0());     // (generic: not merged into a ds_read2_b64)
             for (int kgs = kg0; kgs < kg1; kgs += XPF) {   // (one batch at cfg5: 8 k-groups per wave)
 #pragma unroll
                 for (int i = 0; i < XPF; ++i) {
                     const int kg = kgs + i;
                     if (kg < kg1) {
-                        const floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow4 + 16 * kg);
-                        floatx4 b4 = xpf[i];
-                        float b0 = b4[0], b1 = b4[1], b2 = b4[2], b3 = b4[3];
-                        swap16(b0, b2);                    // rows 1 / 3: t 4, 5 <-> rows 0 / 2: t 2, 3
-                        swap16(b1, b3);
-                        b4 = bon ? (floatx4){b0, b1, b2, b3} : (floatx4){0.f, 0.f, 0.f, 0.f};
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b4[0], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b4[1], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b4[2], xacc, 0, 0, 0);
-                        xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b4[3], xacc, 0, 0, 0);
+                        if constexpr (SPEC) {
+                            const floatx4 a4 = lds_ld4(arow + tof(kg));
+                            const floatx4 b4 = bon ? xpf[i] : (floatx4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], xacc, 0, 0, 0);
+                        } else {
+                            const floatx2 a0 = lds_ld2(arow + 16 * kg), a1 = lds_ld2(arow4 + 16 * kg);
+                            floatx4 b4 = xpf[i];
+                            float b0 = b4[0], b1 = b4[1], b2 = b4[2], b3 = b4[3];
+                            swap16(b0, b2);                // rows 1 / 3: t 4, 5 <-> rows 0 / 2: t 2, 3
+                            swap16(b1, b3);
+                            b4 = bon ? (floatx4){b0, b1, b2, b3} : (floatx4){0.f, 0.f, 0.f, 0.f};
+                            xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b4[0], xacc, 0, 0, 0);
+                            xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b4[1], xacc, 0, 0, 0);
+                            xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b4[2], xacc, 0, 0, 0);
+                            xacc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b4[3], xacc, 0, 0, 0);
+                        }
                     }
                 }
                 if (kgs + XPF < kg1) xload(kgs + XPF);
