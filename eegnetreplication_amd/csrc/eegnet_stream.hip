@@ -1427,9 +1427,11 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                 // its own 4-bank slot (RS / 4 odd) -- conflict-free at one instruction per operand (the
                 // plain t = 16 kg + 4 lk order was 2-way; two ds_read_b64 per operand are conflict-free
                 // but cost more issue than the conflicts did)
+                // (a lane past the last channel reads -- and zeroes -- row li, not row 0: row 0 shares
+                // its 4-bank slot with row 16, which lane li = 0 of the second c-tile reads)
                 const int lo = 64 * (lk & 1) + 4 * (lk >> 1);
                 const float* arow = Eb + (aon ? li : 0) * RS + LP + lo;
-                const float* brow = Xb + (bon ? c : 0) * RS + LP + lo;
+                const float* brow = Xb + (bon ? c : li) * RS + LP + lo;
                 for (int kg = kg0; kg < kg1; ++kg) {
                     const int to = 128 * (kg >> 3) + 8 * (kg & 7);
                     floatx4 a4, b4;
@@ -1451,7 +1453,7 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                 // The +8 halves go through an offset the compiler cannot see: two plain ds_read_b64 8
                 // floats apart merge into one ds_read2_b64, which banks mod 32 in 16-lane groups (2-way)
                 const float* arow = Eb + (aon ? li : 0) * RS + LP + 2 * lk;
-                const float* brow = Xb + (bon ? c : 0) * RS + LP + 2 * lk;
+                const float* brow = Xb + (bon ? c : (li < C ? li : 0)) * RS + LP + 2 * lk;
                 const int o8 = 8 + opaque0();
                 const float* arow8 = arow + o8;
                 const float* brow8 = brow + o8;
