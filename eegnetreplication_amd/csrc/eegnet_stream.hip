@@ -1419,7 +1419,7 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
         if (gemm_on) {
             const int c = ct * 16 + li;
             const bool aon = li < F2, bon = c < C;
-            if constexpr (TT != 0 && TT % 128 == 0) {
+            if constexpr (TT != 0 && TT / 128 >= 2) {
                 // k-group kg of a 128-sample block: lane lk takes the float4 at t = 128 (kg >> 3) +
                 // 8 (kg & 7) + 64 (lk & 1) + 4 (lk >> 1), one ds_read_b128 per operand.  The 16-lane
                 // groups of ds_read_b128 ({0-3, 12-15, 20-27}, ...) pair lk = 0 with 1 and 2 with 3, whose
@@ -1429,11 +1429,14 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                 // but cost more issue than the conflicts did)
                 // (a lane past the last channel reads -- and zeroes -- row li, not row 0: row 0 shares
                 // its 4-bank slot with row 16, which lane li = 0 of the second c-tile reads)
+                // 22×257: the k-groups past the last whole 128-sample block (kg 16: t = 256 and the
+                // zero pad) keep the plain order t = 16 kg + 4 lk, the only 2-way group of the trial
+                constexpr int KGP = 8 * (TT / 128);
                 const int lo = 64 * (lk & 1) + 4 * (lk >> 1);
                 const float* arow = Eb + (aon ? li : 0) * RS + LP + lo;
                 const float* brow = Xb + (bon ? c : li) * RS + LP + lo;
                 for (int kg = kg0; kg < kg1; ++kg) {
-                    const int to = 128 * (kg >> 3) + 8 * (kg & 7);
+                    const int to = kg < KGP ? 128 * (kg >> 3) + 8 * (kg & 7) : 16 * kg + 4 * lk - lo;
                     floatx4 a4, b4;
                     if (EEGNET_LDSX_E == 4) {
                         a4 = (floatx4){0.01f * kg, 0.02f * li, 0.f, 1.f};
