@@ -20,7 +20,8 @@
 //
 // Residency.  The grid barriers need every workgroup resident: grid <= 2 x CUs, <= 128 VGPRs and
 // <= 80 KB of LDS per workgroup (checked on the host with the occupancy query; the multi-launch step
-// runs otherwise).  Every spin is bounded (a timeout sets the error word and lets the kernel finish).
+// runs otherwise).  Every spin is bounded (a timeout sets the sticky error word, the step's loss
+// becomes NaN, and the kernel finishes).
 // Two persistent steps must never run concurrently on one device (they would split the CUs and wait
 // for each other's workgroups): the step is opt-in per call (EEGNET_PERSIST), set by FusedTrainer,
 // whose steps are stream-ordered.
@@ -28,40 +29,19 @@
 namespace eeg {
 
 // ---------------------------------------------------------------------------------------------
-// Grid barrier: 16 arrival words (one per 64-byte line; workgroup w arrives on word w % 16), polled by
-// 16 lanes of wave 0.  Barrier k of a launch completes when word j reaches k x (its workgroup count).
-// The last workgroup to leave the kernel re-arms the words.  Partial rows and column totals are
-// written with agent-scope (sc1) stores and read with sc1 loads, drained before the arrival
-// (MI355X_MICROARCH.md, inter-workgroup visibility: the sc1 form of the release / acquire hand-off).
+// Synchronisation words (one per 64-byte line): the departure counter (the last workgroup out of the
+// kernel re-arms the release word and itself), the sticky error word (a bounded wait timed out: the
+// grid was not co-resident; the last workgroup out then writes NaN into the loss, and the word stays
+// set), and the release word (the grid reduction k of this launch is done: preduce).  Partial rows and
+// column totals are written with agent-scope (sc1) stores and read with sc1 loads, drained before the
+// hand-off (MI355X_MICROARCH.md, inter-workgroup visibility).
 // ---------------------------------------------------------------------------------------------
-constexpr int PS_NARR = 16;          // arrival words
-constexpr int PS_STRIDE = 16;        // unsigned words between arrival words (64 B)
-constexpr int PS_DEP = PS_NARR;      // departure word (index in PS_STRIDE units)
-constexpr int PS_ERR = PS_NARR + 1;  // error word: set when a barrier wait timed out
-constexpr int PS_REL = PS_NARR + 2;  // release word: the grid reduction k of this launch is done
-constexpr int PS_WORDS = (PS_NARR + 3) * PS_STRIDE;
+constexpr int PS_STRIDE = 16;        // unsigned words between synchronisation words (64 B)
+constexpr int PS_DEP = 0;            // departure word (index in PS_STRIDE units)
+constexpr int PS_ERR = 1;            // error word
+constexpr int PS_REL = 2;            // release word
+constexpr int PS_WORDS = 3 * PS_STRIDE;
 constexpr unsigned long long PS_TIMEOUT_TICKS = 100000000ull;   // 1 s of the 100 MHz wall clock
-
-__device__ __forceinline__ void gsync(unsigned* sync, unsigned k, int G, int wg) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's row / total stores drained
-    __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(sync + PS_STRIDE * (wg % PS_NARR), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x < PS_NARR) {
-        const int j = threadIdx.x;
-        const unsigned need = k * (unsigned)(j < G ? (G - j + PS_NARR - 1) / PS_NARR : 0);
-        const unsigned* wj = sync + PS_STRIDE * j;
-        const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(wj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > PS_TIMEOUT_TICKS) {          // not co-resident: give up, flag it
-                __hip_atomic_store(sync + PS_STRIDE * PS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
 
 // fp64 sum over the 64 lanes, fixed butterfly order (every lane gets the total)
 __device__ __forceinline__ double wave_sum_f64(double v) {
@@ -459,8 +439,10 @@ __global__ __launch_bounds__(NTB, WPEB) void k_step(Geo gin, StepArgs a) {
         const unsigned prev = __hip_atomic_fetch_add(a.sync + PS_STRIDE * PS_DEP, 1u, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
         if (prev == (unsigned)G - 1u) {
-            for (int j = 0; j < PS_NARR; ++j)
-                __hip_atomic_store(a.sync + PS_STRIDE * j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // a timed-out wait anywhere in this step (or an earlier one: the word is sticky) makes the
+            // step's loss NaN, so the failure cannot pass unnoticed
+            if (a.loss && __hip_atomic_load(a.sync + PS_STRIDE * PS_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                *a.loss = __builtin_nanf("");
             __hip_atomic_store(a.sync + PS_STRIDE * PS_REL, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.sync + PS_STRIDE * PS_DEP, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
