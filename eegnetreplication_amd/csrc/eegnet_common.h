@@ -656,9 +656,12 @@ __device__ __forceinline__ void x_store(const float (&pf)[PF], int C, int T, int
 // floats apart) put 16 lanes on overlapping banks, a 2-way conflict on every operand read.  Steps
 // 2j, 2j + 1 instead take channels 8j .. 8j + 7 with each half on rows c, c + 4 (4 RS = 16 mod 32:
 // disjoint banks).  Odd KS keeps the plain order.
+#ifndef EEGNET_SPATIAL_PLAIN
+#define EEGNET_SPATIAL_PLAIN 0      // (A/B builds: 1 = the plain channel order)
+#endif
 template <int KS>
 __device__ __forceinline__ int spatial_ch(int s, int lk) {
-    if constexpr (KS % 2 == 0) {
+    if constexpr (KS % 2 == 0 && !EEGNET_SPATIAL_PLAIN) {
         // step part (compile-time: an immediate LDS offset) + lane part (in the base address)
         return (8 * (s >> 1) + 2 * (s & 1)) + ((lk >> 1) + 4 * (lk & 1));
     } else {
@@ -686,7 +689,7 @@ __device__ __forceinline__ void spatial_mfma(const float* Xs, const float (&aw)[
                                              int NT16, int RS, int LP, int wave, int lane) {
     const int li = lane & 15, lk = lane >> 4;
     int ks = (C + 3) >> 2;
-    if constexpr (KS % 2 == 0) ks = (ks + 1) & ~1;     // spatial_ch: steps 2j, 2j + 1 hold 8 channels
+    if constexpr (KS % 2 == 0 && !EEGNET_SPATIAL_PLAIN) ks = (ks + 1) & ~1;   // spatial_ch: steps 2j, 2j + 1 hold 8 channels
     const int cl = spatial_ch<KS>(0, lk);
     const float* xcol = Xs + LP + li + cl * RS;
     for (int n = wave; n < NT16; n += NW) {
