@@ -105,6 +105,14 @@ __device__ __forceinline__ void spatial_load5(const float* __restrict__ xb, floa
 #pragma unroll
     for (int s = 0; s < KSW; ++s) bv[s] = xb[(size_t)(4 * s + lk) * 512 + 16 * (wave + NWW * m) + li];
 }
+// k-steps [s0, s1) of tile m's B operands only
+__device__ __forceinline__ void spatial_load5r(const float* __restrict__ xb, float (&bv)[KSW], int m, int wave, int lane,
+                                               int s0, int s1) {
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < KSW; ++s)
+        if (s >= s0 && s < s1) bv[s] = xb[(size_t)(4 * s + lk) * 512 + 16 * (wave + NWW * m) + li];
+}
 __device__ __forceinline__ void spatial_mfma5(const float (&bv)[KSW], const float* awl, float* Ss, int RS, int LP, int m,
                                               int wave, int lane) {
     const int li = lane & 15, lk = lane >> 4;
@@ -224,6 +232,9 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     __syncthreads();                                   // zero fill done before the first slice lands
     if (b0 < b1 && nc > 0) stage_slice(x + ((size_t)b0 * C + c0) * T, nc, T, RS, LP, Xg, tid, wave, lane);
     barrier_vm<0>();                                   // the first slice landed (asm DMA: explicit vmcnt)
+    constexpr int KPF = KSW / 2;                       // cfg5: tile 0's first KPF k-steps come a trial ahead
+    if constexpr (SPEC)
+        if (b0 < b1) spatial_load5r(x + (size_t)b0 * C * T, bv5, 0, wave, lane, 0, KPF);
     TRACE(g, 0, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
@@ -255,7 +266,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
         if constexpr (SPEC) {
             Xg = sm + ((b - b0) & 1) * g.CPC * RS;
             Ss = sm + 2 * g.CPC * RS + ((b - b0) & 1) * 16 * RS;
-            spatial_load5(x + (size_t)b * C * T, bv5, 0, wave, lane);
+            spatial_load5r(x + (size_t)b * C * T, bv5, 0, wave, lane, KPF, KSW);
             spatial_load5(x + (size_t)b * C * T, bw5, 1, wave, lane);
             // the previous trial's s / v plane stores go out after this trial's operand loads, so
             // waiting for those loads (vmcnt is in order) does not wait for the stores to drain: at
@@ -264,11 +275,10 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
             // prefetch now hold the deferred v octet)
             if (bd >= 0) plane_stores(bd);
             spatial_mfma5(bv5, awl, Ss, RS, LP, 0, wave, lane);
+            if (bn < b1) spatial_load5r(x + (size_t)bn * C * T, bv5, 0, wave, lane, 0, KPF);
             spatial_mfma5(bw5, awl, Ss, RS, LP, 1, wave, lane);
-            // s rows complete; this trial's slice (DMA'd in the previous trial, before the operand
-            // loads) landed: everything but the SV_ST youngest (the deferred stores)
             TRACE_PH(g, 0, 0, tph_);
-            barrier_vm<SV_ST>();
+            barrier_vm<SV_ST + KPF>();
         } else {
             spatial_chunk(x + (size_t)b * C * T, awl, Ss, C, T, NT16, RS, LP, wave, lane);
         }
