@@ -37,22 +37,6 @@ ALG_BYTES_PER_TRIAL = 45_056     # x read twice
 CFG4_GLOBAL_BATCH = 65536        # BASELINE configs[3]
 
 
-STEP_KERNEL = "k_step"      # the persistent step: all five passes in one launch (eegnet_persist.hip)
-
-
-def with_step_kernel(alg, ab=None):
-    """The per-pass tables plus the persistent step kernel, whose work per trial is the whole step's:
-    (sum of the passes' FLOPs, sum of their bytes); its algorithmic bytes are the step's (x twice +
-    the label).  The sums over the passes stay over ``alg`` itself."""
-    out = dict(alg)
-    out[STEP_KERNEL] = (sum(v[0] for v in alg.values()), sum(v[1] for v in alg.values()))
-    if ab is None:
-        return out
-    ab2 = dict(ab)
-    ab2[STEP_KERNEL] = sum(ab.values())
-    return out, ab2
-
-
 def kernel_alg_bytes(C=22, T=256, wide=False):
     """SURVEY 8(d)'s algorithmic HBM bytes per trial, attributed to the kernels that need them: x
     is read once for the forward (pass A) and once for the weight gradients (pass E); the labels
@@ -117,7 +101,7 @@ def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
 # waves per SIMD each kernel's launch configuration admits (workgroup size x workgroups per CU / 4 SIMDs)
 LAUNCH_WAVES_PER_SIMD = {"k_pass_a": 4, "k_pass_b": 4, "k_pass_c": 4, "k_pass_d": 2, "k_pass_e": 4,
                          "k_infer": 4, "k_wpass_a": 4, "k_wpass_b": 4, "k_wpass_b2": 2, "k_wpass_c": 2,
-                         "k_wpass_d": 2, "k_wpass_e": 4, "k_infer_bf16_cfg5": 4, "k_step": 4}
+                         "k_wpass_d": 2, "k_wpass_e": 4, "k_infer_bf16_cfg5": 4}
 
 
 def load_util():
@@ -671,7 +655,7 @@ def bench_cfg4(dev, rank, world, G, steps, warmup, barrier, nx=2):
     for i in range(warmup):
         tr.step(xs[i % nx], ys[i % nx])
     alg = kernel_algorithmic(C, T)
-    alg_k, ab_k = with_step_kernel(alg, kernel_alg_bytes(C, T))
+    alg_k, ab_k = alg, kernel_alg_bytes(C, T)
     dt, table, dom, dk = timed_steps(tr, xs, ys, steps, alg_k, B, barrier)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
@@ -752,7 +736,7 @@ def main():
     for i in range(args.warmup):
         trainer.step(xs[i % args.nx], ys[i % args.nx])
     alg = kernel_algorithmic(C, T)
-    alg_k, ab_k = with_step_kernel(alg, kernel_alg_bytes(C, T))
+    alg_k, ab_k = alg, kernel_alg_bytes(C, T)
     dt, table, dom, dk = timed_steps(trainer, xs, ys, args.steps, alg_k, B, barrier, prof)
     loss = float(trainer.loss.item())
 
@@ -835,8 +819,7 @@ def main():
                        "channels": C, "parallelism": f"dp{world}"},
             "roofline": roof,
             "step_roofline": step_roofline(impl_flop, ALG_BYTES_PER_TRIAL, impl_bytes, trials_per_s / world,
-                                           pmc.get(STEP_KERNEL, {}).get("hbm_bytes_per_launch")
-                                           if dom == STEP_KERNEL else pmc_step_bytes(pmc, alg), B),
+                                           pmc_step_bytes(pmc, alg), B),
             "cpu_baseline": cpu,
             "hbm_fraction": round(ALG_BYTES_PER_TRIAL * trials_per_s / world / (PEAK_HBM_GBS * 1e9), 4),
             "step_fp32_frac": round(impl_flop * trials_per_s / world / (PEAK_FP32_TFLOPS * 1e12), 4),

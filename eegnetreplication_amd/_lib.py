@@ -137,7 +137,7 @@ def workspace_bytes(d: Dims) -> int:
 
 KERNEL_IDS = ("k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e", "k_adam", "k_infer",
               "memset_tickets", "k_infer_bf16", "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c",
-              "k_wpass_d", "k_wpass_e", "k_winfer", "k_coltail", "k_xstats", "k_step")
+              "k_wpass_d", "k_wpass_e", "k_winfer", "k_coltail", "k_xstats")
 
 
 def profile_enable(on: bool = True, kernels=None):

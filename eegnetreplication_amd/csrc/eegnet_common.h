@@ -118,27 +118,6 @@ __device__ __forceinline__ Geo geo_w(const Geo& gin) {
     return g;
 }
 
-// Compile-time EEGNet-8,2 geometry at 22 x 256 / 22 x 257 (K1 = 32) for the persistent step (k_step,
-// eegnet_persist.hip): the shape fields make_geo computes for those dims.  k_step works on a copy of its
-// Geo with these overwritten, so the fields are constants and take no SGPRs for the whole kernel (one
-// kernel holding all five passes ran out of SGPRs otherwise: 160 spilled).  The host launches k_step
-// only when its run-time geometry equals these field for field (eegnet_host.hip persist_ok).
-#define EEG_SHAPE_N22(X)                                                                            \
-    X(C, 22) X(F1, 8) X(D, 2) X(F2, 16) X(K1, 32) X(P, 15) X(R, 16) X(T1, 64) X(T2, 8) X(NF, 128)    \
-    X(LP, 16) X(RS2, 80) X(RSW, 92) X(CK, 24) X(NCT, 2) X(nH, 136) X(nTl, 120) X(nedge, 287)       \
-    X(o_w1, 0) X(o_g1, 256) X(o_b1, 264) X(o_ws, 272) X(o_g2, 624) X(o_b2, 640) X(o_w2, 656)        \
-    X(o_W3, 912) X(o_g3, 1168) X(o_b3, 1184) X(o_Wfc, 1200) X(o_bfc, 1712) X(nparam, 1716)        \
-    X(nA, 352) X(nB, 32) X(nC, 549) X(nD, 544) X(nE, 640) X(QR, 8) X(wide, 0) X(defer, 0)
-#define EEG_SHAPE_N256(X) EEG_SHAPE_N22(X) X(T, 256) X(RS, 292) X(TQ, 64) X(NT16, 16) X(NKG, 16) X(XP, 256)
-#define EEG_SHAPE_N257(X) EEG_SHAPE_N22(X) X(T, 257) X(RS, 308) X(TQ, 65) X(NT16, 17) X(NKG, 17) X(XP, 257)
-template <int TT>
-__host__ __device__ __forceinline__ void shape_n22(Geo& g) {
-#define EEG_SET_(f, v) g.f = v;
-    if constexpr (TT == 256) { EEG_SHAPE_N256(EEG_SET_) }
-    else { EEG_SHAPE_N257(EEG_SET_) }
-#undef EEG_SET_
-}
-
 // timeline stamps: wall clock (100 MHz) at kernel phase boundaries, shader-clock phase sums (loop)
 constexpr int TR_SLOTS = 16, TR_MAXWG = 2048;
 enum TraceEv { TR_ENTRY = 0, TR_PRO, TR_LOOP, TR_PUB, TR_GRP, TR_TOP, TR_FIN, TR_PH0 = 8 };

@@ -27,7 +27,6 @@ constexpr size_t CNT_BYTES = (size_t)TK_COUNT * NCNT * 4;     // 800 B, a multip
 
 struct WsLayout {
     size_t cnt, partA, partB, partC, partD, partE, sums, stats, coef, d2, E1, E2, dp2, dl, s, v, q3, r3;
-    size_t ptot, psync, pcoef, pstats, pgrads;   // the persistent step (k_step, eegnet_persist.hip)
     size_t total;
 };
 
@@ -57,37 +56,33 @@ static void b2_lds(Geo* g, int nw) {
     g->ldsWD = std::max(b2 + g->F2P * g->RB + nf4 + 2 * g->F2 * TQ1, tailw(g->nD, 0));
 }
 
+// Launch-shape choices fixed at build time (the shipped library reads no environment: kernel choice and
+// grids are functions of the dims alone).  A/B experiments build variants with -D (tools/ab.sh).
+//
 // Block-2 passes C / D of the F2 <= 16 step: one trial per wave (k_pass_c / k_pass_d, the default)
-// or whole-trial 256-thread workgroups (the wide path's k_wpass_c / k_wpass_d, EEGNET_B2=1).  Before
+// or whole-trial 256-thread workgroups (the wide path's k_wpass_c / k_wpass_d, -DEEGNET_B2=1).  Before
 // pass B stored the q / r planes the whole-trial kernels won at small per-launch grids (batch 64,
 // fold-indexed launches); with the planes the one-trial-per-wave kernels win the fold-indexed
 // real-protocol leg (6.5 M against 5.9 M trials/s) and lose 3-7% on a lone batch of 64.  One rule
 // for every launch keeps a fold-indexed step bit-identical to the same fold's FusedTrainer step.
-static bool use_b2_narrow(const Geo&) {
-    static int v = -2;
-    if (v == -2) { const char* e = getenv("EEGNET_B2"); v = e ? (e[0] == '1' ? 1 : 0) : 0; }
-    return v == 1;
-}
+#ifndef EEGNET_B2
+#define EEGNET_B2 0
+#endif
+static bool use_b2_narrow(const Geo&) { return EEGNET_B2 == 1; }
 
-// workgroups per CU slot of the streaming passes A / B / E (EEGNET_GRIDS_MULT, experiments): with more
-// workgroups than resident slots the dispatcher refills a CU's early-finishing slot, so the two
-// resident workgroups' skew turns into load balance
-static int env_mult(const char* name) {
-    const char* e = getenv(name);
-    const int v = e ? atoi(e) : 1;
-    return (v >= 1 && v <= 8) ? v : 1;
-}
-static int grid_mult() {
-    static int m = 0;
-    if (m == 0) m = env_mult("EEGNET_GRIDS_MULT");
-    return m;
-}
-// the same for passes C / D (EEGNET_GRIDC_MULT)
-static int grid_mult_cd() {
-    static int m = 0;
-    if (m == 0) m = env_mult("EEGNET_GRIDC_MULT");
-    return m;
-}
+// workgroups per CU slot of the streaming passes A / B / E (-DEEGNET_GRIDS_MULT=n, experiments): with
+// more workgroups than resident slots the dispatcher refills a CU's early-finishing slot, so the two
+// resident workgroups' skew turns into load balance; the same for passes C / D (-DEEGNET_GRIDC_MULT)
+#ifndef EEGNET_GRIDS_MULT
+#define EEGNET_GRIDS_MULT 1
+#endif
+#ifndef EEGNET_GRIDC_MULT
+#define EEGNET_GRIDC_MULT 1
+#endif
+static_assert(EEGNET_GRIDS_MULT >= 1 && EEGNET_GRIDS_MULT <= 8 && EEGNET_GRIDC_MULT >= 1 && EEGNET_GRIDC_MULT <= 8,
+              "grid multipliers are 1..8");
+static constexpr int grid_mult() { return EEGNET_GRIDS_MULT; }
+static constexpr int grid_mult_cd() { return EEGNET_GRIDC_MULT; }
 
 // the compile-time shape of the narrow passes (EEG_DISPATCH) whose x loads honour a row pitch: 22 x 257
 // (the recordings), whose 257-float rows are not 16-byte units; 22 x 256 rows already are, and its
@@ -250,9 +245,8 @@ static WsLayout make_layout(const Geo& g) {
     L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
     L.partA = take((size_t)g.gridS * g.nA * 4);
     L.partB = take((size_t)std::max(g.gridS, g.grid) * g.nB * 4);
-    // (k_step runs passes C / D on the streaming grid)
-    L.partC = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridS) * g.nC * 4);
-    L.partD = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridS) * g.nD * 4);
+    L.partC = take((size_t)std::max(g.grid, g.gridB2) * g.nC * 4);
+    L.partD = take((size_t)std::max(g.grid, g.gridB2) * g.nD * 4);
     L.partE = take((size_t)g.gridS * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
     L.sums = take((size_t)nmax * 8 * NGRPMAX);
@@ -268,13 +262,6 @@ static WsLayout make_layout(const Geo& g) {
     // C (r) and D (q, r) instead of recomputing them from d2
     L.q3 = take(per);
     L.r3 = take(per);
-    // the persistent step: column totals, barrier words (zero-filled with the workspace, re-armed by
-    // every launch), and every workgroup's coefficient block / fin1 statistics / gradient copy
-    L.ptot = take((size_t)nmax * 8);
-    L.psync = take((size_t)PS_WORDS * 4);
-    L.pcoef = take((size_t)g.gridS * CF_COUNT * CSTR * 4);
-    L.pstats = take((size_t)g.gridS * (g.F1 * g.K1 + g.K1) * 8);
-    L.pgrads = take((size_t)g.gridS * g.nparam * 4);
     L.total = o;
     return L;
 }
@@ -296,12 +283,11 @@ static void set_key(Geo* g, uint64_t seed, uint64_t offset) {
 
 // ---- optional per-kernel device timing (bench / roofline), off by default ----
 enum KernelId { KID_A = 0, KID_B, KID_C, KID_D, KID_E, KID_ADAM, KID_INFER, KID_MEMSET, KID_INFER_BF16,
-                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_CTAIL, KID_XSTATS, KID_STEP,
-                KID_COUNT };
+                KID_WA, KID_WB, KID_WB2, KID_WC, KID_WD, KID_WE, KID_WINFER, KID_CTAIL, KID_XSTATS, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c", "k_pass_d", "k_pass_e",
                                               "k_adam", "k_infer", "memset_tickets", "k_infer_bf16",
                                               "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c", "k_wpass_d",
-                                              "k_wpass_e", "k_winfer", "k_coltail", "k_xstats", "k_step"};
+                                              "k_wpass_e", "k_winfer", "k_coltail", "k_xstats"};
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { unsigned mask = 0; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
@@ -377,49 +363,7 @@ static void ensure_attrs() {
     hipFuncSetAttribute((const void*)k_xstats<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     set_attrs_shape<32, 22, 256, 16>();
     set_attrs_shape<32, 22, 257, 16>();
-    hipFuncSetAttribute((const void*)k_step<32, 22, 256, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    hipFuncSetAttribute((const void*)k_step<32, 22, 257, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     g_attr_done = true;
-}
-
-// ---- the persistent step (k_step, eegnet_persist.hip) ----
-// LDS (floats) of k_step: the largest phase, pass C / D re-laid for 8-wave workgroups, the grid
-// reductions with their finalize scratch (fin1 after A, fin5 after E)
-static int persist_lds(const Geo& g) {
-    const int nf4 = rup(g.NF, 4), nw = NTB / 64;
-    int l = std::max(std::max(g.ldsA, g.ldsB), g.ldsE);
-    l = std::max(l, std::max(nw * nf4, nw * g.nC));
-    l = std::max(l, std::max(pd_lds_floats(), nw * g.nD));
-    l = std::max(l, 2 * (preduce_doubles(g.nA) + fin1_scratch_doubles(g.K1, g.F1, g.F2, g.C)));
-    l = std::max(l, 2 * (preduce_doubles(g.nE) + fin5_scratch_doubles(g.K1, g.F1, g.o_g2)));
-    l = std::max(l, 16 * g.RS + 2 * preduce_doubles(g.nD));
-    l = std::max(l, 2 * (preduce_doubles(g.nC)));
-    return l;
-}
-// Whether a step of geometry g may run as k_step: the compile-time EEGNet-8,2 shapes, and a grid every
-// workgroup of which is resident at once (two per CU: the occupancy query with k_step's real
-// registers and LDS, cached per shape) -- the grid barriers need it
-static bool persist_ok(const Geo& g) {
-    if (g.wide || g.defer || g.K1 != 32 || g.C != 22 || (g.T != 256 && g.T != 257) || g.F1 != 8 || g.D != 2) return false;
-    if (g.XP != g.T) return false;                       // (the pitched 22 x 257 rows are the fold launches')
-    {   // the compile-time geometry k_step overwrites its Geo with (EEG_SHAPE_N22) must be make_geo's
-#define EEG_EQ_(f, v) && g.f == v
-        const bool same = g.T == 256 ? (true EEG_SHAPE_N256(EEG_EQ_)) : (true EEG_SHAPE_N257(EEG_EQ_));
-#undef EEG_EQ_
-        if (!same) return false;
-    }
-    if (const char* e = getenv("EEGNET_PERSIST")) if (e[0] == '0') return false;
-    static int ok[2] = {-1, -1};
-    const int i = g.T == 256 ? 0 : 1;
-    if (ok[i] < 0) {
-        const int lds = persist_lds(g) * 4;
-        int nb = 0;
-        const void* f = i == 0 ? (const void*)k_step<32, 22, 256, 16> : (const void*)k_step<32, 22, 257, 16>;
-        ensure_attrs();
-        if (lds > 80 * 1024 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, NTB, lds) != hipSuccess) nb = 0;
-        ok[i] = nb >= WGPC ? 1 : 0;
-    }
-    return ok[i] == 1 && g.gridS <= WGPC * device_cus();
 }
 
 // compile-time shape specialisations (the benchmark and real-data configurations); any other shape
@@ -631,6 +575,9 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     return 0;
 }
 
+#ifndef EEGNET_BF16_V1
+#define EEGNET_BF16_V1 0
+#endif
 // geometry of the bf16 eval kernel (eegnet_infer_bf16.hip)
 static float* g_bf16_dbg = nullptr;     // eegnet_debug_bf16 (debug builds only)
 
@@ -842,10 +789,9 @@ int eegnet_forward_eval_bf16(const eegnet_dims* dims, const float* params, const
     const dim3 grid(std::min(g.B, device_cus())), blk(NTI);
     PROF(KID_INFER_BF16);
     if (same_geo_bf16(g, kGeoCfg5)) {
-        // time-chunked cfg5 kernel, two workgroups per CU (eegnet_infer_bf16c.hip); EEGNET_BF16_V1=1
-        // keeps the whole-trial kernel (A/B measurements)
-        static const bool v1 = getenv("EEGNET_BF16_V1") && getenv("EEGNET_BF16_V1")[0] == '1';
-        if (v1) hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
+        // time-chunked cfg5 kernel, two workgroups per CU (eegnet_infer_bf16c.hip); a -DEEGNET_BF16_V1=1
+        // build keeps the whole-trial kernel (A/B measurements)
+        if (EEGNET_BF16_V1 == 1) hipLaunchKernelGGL((k_infer_bf16<8, true>), grid, blk, g.lds, s, g, params, bn_buffers, x, logits);
         else hipLaunchKernelGGL(k_infer_bf16_cfg5, dim3(std::min(g.B, 2 * device_cus())), dim3(c5::NT), c5::LDS, s,
                                 g, params, bn_buffers, x, logits);
         LAUNCH_CHECK("k_infer_bf16(cfg5)");
@@ -888,6 +834,9 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     if (int r = check_ptrs(x, "x", labels, "labels")) return r;
     if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
     if (adam_state && !step) return fail(EEGNET_EINVAL, "step is NULL");
+    if (flags & ~(EEGNET_NO_CLAMP | EEGNET_KEY_FROM_STEP))
+        return fail(EEGNET_EINVAL, "unknown flags 0x%x (bit 4, the ABI-5 persistent step, was retired in ABI 6)",
+                    flags & ~(EEGNET_NO_CLAMP | EEGNET_KEY_FROM_STEP));
     g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
     g.drop = g.p > 0.f ? 1 : 0;
     set_key(&g, seed, offset);
@@ -899,31 +848,6 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     const WsLayout L = make_layout(g);
     hipStream_t s = (hipStream_t)stream;
     char* w = (char*)ws;
-    if ((flags & EEGNET_PERSIST) && persist_ok(g)) {
-        // the whole step as ONE launch of a co-resident grid (eegnet_persist.hip)
-        StepArgs a;
-        memset(&a, 0, sizeof(a));
-        a.x = x; a.labels = labels; a.params = params; a.bn = bn_buffers; a.nbt = num_batches_tracked;
-        a.grads = grads; a.adam_m = adam_state; a.adam_v = adam_state ? adam_state + g.nparam : nullptr;
-        a.step = step; a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.loss = loss; a.logits = logits;
-        a.cmode = PC_BWD | PC_CE | (logits ? PC_LOGITS : 0);
-        a.s = (float*)(w + L.s); a.v = (float*)(w + L.v); a.d2 = (float*)(w + L.d2); a.E1 = (float*)(w + L.E1);
-        a.E2 = (float*)(w + L.E2); a.q3 = (float*)(w + L.q3); a.r3 = (float*)(w + L.r3); a.dl = (float*)(w + L.dl);
-        a.dp2 = (float*)(w + L.dp2);
-        a.partA = (float*)(w + L.partA); a.partB = (float*)(w + L.partB); a.partC = (float*)(w + L.partC);
-        a.partD = (float*)(w + L.partD); a.partE = (float*)(w + L.partE);
-        a.tot = (double*)(w + L.ptot); a.sync = (unsigned*)(w + L.psync);
-        a.cnt = (unsigned*)(w + L.cnt); a.part2 = (double*)(w + L.sums);
-        a.wcoef = (float*)(w + L.pcoef); a.wstats = (double*)(w + L.pstats); a.wgrads = (float*)(w + L.pgrads);
-        const size_t lds = (size_t)persist_lds(g) * 4;
-        {
-            PROF(KID_STEP);
-            if (g.T == 256) hipLaunchKernelGGL((k_step<32, 22, 256, 16>), dim3(g.gridS), dim3(NTB), lds, s, g, a);
-            else hipLaunchKernelGGL((k_step<32, 22, 257, 16>), dim3(g.gridS), dim3(NTB), lds, s, g, a);
-        }
-        LAUNCH_CHECK("k_step");
-        return 0;
-    }
     int r = g.K1 == 32 ? run_forward<32>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s)
                        : run_forward<64>(g, L, w, params, bn_buffers, x, nullptr, 1, num_batches_tracked, s);
     if (r) return r;
@@ -1023,21 +947,21 @@ int eegnet_stage_sums(const eegnet_dims* dims, int pass, size_t* offset_bytes, i
 }  // extern "C"
 
 // trials per workgroup of the fold-indexed launches: streaming passes A / B / E, passes C / D, the
-// whole-trial block-2 passes (EEGNET_B2=1); EEGNET_FOLD_TPW="s,c,b2" overrides them (sweeps).  Chosen
-// by tools/fold_tpw_sweep.py over 90, 36 and 12 resident folds of batch 64 (22 x 257):
-// 4,8,2 trains 12 folds per GPU (cfg3: 90 folds over 8 GPUs) 1.9x faster than the grid 90 folds on
-// one GPU prefer (13,32,6), at 7 % less on those 90.
+// whole-trial block-2 passes (-DEEGNET_B2=1); a -DEEGNET_FOLD_TPW_S / _C / _B2 build overrides them
+// (sweeps).  Chosen by tools/fold_tpw_sweep.py over 90, 36 and 12 resident folds of batch 64 (22 x 257;
+// DESIGN 6.1): 4,8,2 trains 12 folds per GPU (cfg3: 90 folds over 8 GPUs) 1.9x faster than the grid
+// 90 folds on one GPU prefer (13,32,6), at 7 % less on those 90.
+#ifndef EEGNET_FOLD_TPW_S
+#define EEGNET_FOLD_TPW_S 4
+#endif
+#ifndef EEGNET_FOLD_TPW_C
+#define EEGNET_FOLD_TPW_C 8
+#endif
+#ifndef EEGNET_FOLD_TPW_B2
+#define EEGNET_FOLD_TPW_B2 2
+#endif
 static void fold_tpw(int* s, int* c, int* b2) {
-    static int v[3] = {0, 0, 0};
-    if (v[0] == 0) {
-        int a = 4, b = 8, d = 2;
-        if (const char* e = getenv("EEGNET_FOLD_TPW")) {
-            int x = 0, y = 0, z = 0;
-            if (sscanf(e, "%d,%d,%d", &x, &y, &z) == 3 && x > 0 && y > 0 && z > 0) { a = x; b = y; d = z; }
-        }
-        v[1] = b; v[2] = d; v[0] = a;
-    }
-    *s = v[0]; *c = v[1]; *b2 = v[2];
+    *s = EEGNET_FOLD_TPW_S; *c = EEGNET_FOLD_TPW_C; *b2 = EEGNET_FOLD_TPW_B2;
 }
 
 extern "C" {

@@ -167,8 +167,8 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
             if (i < F2 * W2R) W2p[i] = __builtin_bit_cast(uint16_t, (__bf16)((k >= 0 && k < K2) ? w2v[u] : 0.f));
         }
     }
-    // s rows: positions 96..111 meet only zero taps but must be finite (the z image of a previous
-    // trial leaves finite values there); a rows: 'same' pads of the dw16
+    // s rows: positions 96..111 meet only zero taps but must be finite (re-zeroed after every trial's
+    // tail, whose z image lies over them); a rows: 'same' pads of the dw16
     for (int i = tid; i < 2 * F2 * SROW / 2; i += NT) reinterpret_cast<uint32_t*>(smc + OFF_S)[i] = 0u;
     for (int i = tid; i < F2 * AROW / 2; i += NT) reinterpret_cast<uint32_t*>(Ai)[i] = 0u;
 
@@ -408,6 +408,15 @@ __global__ __launch_bounds__(c5::NT, 4) void k_infer_bf16_cfg5(GeoI g, const flo
         PH_(6);
         barrier_lds_c();                                   // logit partials complete; z image consumed
         PH_(4);
+        // the z image lay over both s buffers: re-zero each s row's positions 96..111 (bytes 192..223,
+        // read by the FIR with zero taps only), so a non-finite z of this trial cannot reach the next
+        // trial's FIR as 0 * Inf (trials are independent in the reference).  One 8-byte store per
+        // thread: 2 buffers x 64 rows x 4; ordered before the next trial's FIR by its chunk barriers.
+        static_assert(2 * F2 * 4 == NT, "one 8-byte pad store per thread");
+        {
+            const int row = tid >> 2, part = tid & 3;     // row 0..127 over both buffers
+            *reinterpret_cast<uintx2*>(smc + OFF_S + row * (2 * SROW) + 192 + 8 * part) = uintx2{0u, 0u};
+        }
         if (tid < NCLS) {
             float a = prm[g.o_bfc + tid];
             for (int w = 0; w < NW; ++w) a += Lg[w * NCLS + tid];

@@ -38,7 +38,6 @@
 #include "eegnet_finalize.hip"
 #include "eegnet_stream.hip"
 #include "eegnet_passes.hip"
-#include "eegnet_persist.hip"
 #include "eegnet_wide.hip"
 #include "eegnet_infer_bf16.hip"
 #include "eegnet_infer_bf16c.hip"

@@ -142,9 +142,7 @@ __device__ __forceinline__ void bn3_rows(const float* coef, int F2, const float 
 // Per-wave LDS: Hs [NF] -- the flattened head features (model.py:75 Flatten order), then their
 // gradients.
 // ================================================================================================
-// PERSIST (k_step): the workgroup's trials are its streaming-pass range (trial_range), dealt over its
-// waves, so the r plane rows it reads are the ones its own pass B wrote; `hook` runs before the loop
-template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST, class Hook>
+template <int K1, int CC, int TT, int FF, bool FOLD>
 __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restrict__ prm,
                                             const float* coef,    // the finalize writes it: no __restrict__
                                             const float* __restrict__ r3g,
@@ -153,7 +151,7 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
                                             const int64_t* __restrict__ labels,
                                             float* __restrict__ logits, float* __restrict__ dlout,
                                             float* __restrict__ part, int mode, FinArgs fa, const FoldCall& fc,
-                                            float* sm, const Hook& hook) {
+                                            float* sm) {
     EEG_DIMS(g);
     TRACE(g, 2, TR_ENTRY);
     unsigned dk1;
@@ -197,17 +195,7 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
     for (int j = 0; j < 2 * F2MAX; ++j) sdz[j] = 0.f;
     float bacc[NCLS] = {0.f, 0.f, 0.f, 0.f}, lossacc = 0.f;
     const float invB = 1.0f / (float)g.Bn;
-    int bfirst, bstop, bstep;
-    if constexpr (PERSIST) {
-        trial_range(g, bfirst, bstop);
-        bfirst += wave;
-        bstep = nw;
-    } else {
-        bfirst = blockIdx.x * nw + wave;
-        bstop = g.B;
-        bstep = gridDim.x * nw;
-    }
-    hook();                                        // (k_step: BN3's statistics of this step)
+    const int bfirst = blockIdx.x * nw + wave, bstop = g.B, bstep = gridDim.x * nw;
 
     TRACE(g, 2, TR_PRO);
     TRACE_DECL();
@@ -351,10 +339,8 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
     float* row = part + (size_t)blockIdx.x * g.nC;
     for (int c = tid; c < g.nC; c += blockDim.x) pub(row + c, wave_rows_sum<NTH / 64>(red, nw, g.nC, c));
     TRACE_PS(g, 11);
-    if constexpr (!PERSIST) {
-        double* dsm = (double*)sm;
-        if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
-    }
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nC, fa, dsm)) { fin3(g, prm, dsm + 2, fa); TRACE(g, 2, TR_FIN); }
 }
 
 template <int K1, int CC, int TT, int FF, bool FOLD = false>
@@ -367,8 +353,7 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
                                                 float* __restrict__ logits, float* __restrict__ dlout,
                                                 float* __restrict__ part, int mode, FinArgs fa, FoldCall fc) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    pass_c_body<K1, CC, TT, FF, FOLD, false>(g, prm, coef, r3g, mask3, dlin, labels, logits, dlout, part, mode, fa,
-                                             fc, sm, NoHook{});
+    pass_c_body<K1, CC, TT, FF, FOLD>(g, prm, coef, r3g, mask3, dlin, labels, logits, dlout, part, mode, fa, fc, sm);
 }
 
 // ================================================================================================

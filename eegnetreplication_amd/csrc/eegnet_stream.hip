@@ -232,18 +232,7 @@ __device__ __forceinline__ void load_taps(const Geo& g, const float* __restrict_
 //   hs / ts = head / tail sample sums       (window-sum corrections)
 //   Sv, Sv2 = sum v, sum v^2 per row o      (BN2: y2 = a1 v + c1 W)
 // ================================================================================================
-// No-op prologue hook of the stand-alone pass kernels.  The persistent step kernel (k_step,
-// eegnet_persist.hip) passes one that waits for the previous phase's grid reduction and runs its
-// finalize, called where each pass first reads the coefficients -- after the first trial's data loads
-// are in flight.
-struct NoHook {
-    __device__ __forceinline__ void operator()() const {}
-};
-
-// PERSIST: the body of one phase of the persistent step kernel (k_step): it publishes its partial row
-// and returns; k_step runs the grid reduction and the finalize.  Otherwise the stand-alone pass, which
-// ends in the ticketed reduction + finalize (grid_reduce).
-template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST>
+template <int K1, int CC, int TT, int FF, bool FOLD>
 __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restrict__ prm,
                                             const float* __restrict__ x, float* __restrict__ sg,
                                             float* __restrict__ vg, float* __restrict__ part,
@@ -270,7 +259,7 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
     }
     // every pass re-arms its own tickets when it finishes; pass A also clears those of the later
     // passes of this call (stream order), so a call never depends on how the previous one ended
-    if (!PERSIST && blockIdx.x == 0 && threadIdx.x < (TK_PASSES - 1) * NCNT)
+    if (blockIdx.x == 0 && threadIdx.x < (TK_PASSES - 1) * NCNT)
         __hip_atomic_store(fa.cnt + NCNT + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     constexpr int NTS = FF ? 1 : RPW;
     constexpr int NEI = G_::template nei<NTB>();
@@ -660,7 +649,7 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
         if (ea[i] != -2 && tid + NTB * i < g.nedge) pub(row + (K1 + 1 + tid + NTB * i), eacc[i]);
     }
     }
-    if constexpr (!PERSIST) {
+    {
         double* dsm = (double*)sm;
         Fin1Stage f1;                              // fin1's inputs, before the ticket (Fin1Stage)
         if (!g.defer) fin1_load(g, prm, fa, f1);
@@ -677,7 +666,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_a(Geo g, const float* __rest
                                                       float* __restrict__ vg, float* __restrict__ part,
                                                       FinArgs fa, FoldCall fc) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    pass_a_body<K1, CC, TT, FF, FOLD, false>(g, prm, x, sg, vg, part, fa, fc, sm);
+    pass_a_body<K1, CC, TT, FF, FOLD>(g, prm, x, sg, vg, part, fa, fc, sm);
 }
 
 // ================================================================================================
@@ -794,7 +783,7 @@ __global__ __launch_bounds__(NTB) void k_xstats(Geo g, long long n, const float*
 // part row: [Sr F2][Sr2 F2]
 // LDS: d2 rows (pad LP2) | q rows x 2 (alternate trials) | weight table [w2 F2MAX x 16][W3 F2MAX x F2MAX]
 // ================================================================================================
-template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST, class Hook>
+template <int K1, int CC, int TT, int FF, bool FOLD>
 __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restrict__ prm,
                                             const float* coef,    // the finalize writes it: no __restrict__
                                             const float* __restrict__ vg,
@@ -802,7 +791,7 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
                                             float* __restrict__ d2g, float* __restrict__ E1g,
                                             float* __restrict__ E2g, float* __restrict__ q3g,
                                             float* __restrict__ r3g, float* __restrict__ part,
-                                            FinArgs fa, const FoldCall& fc, float* sm, const Hook& hook) {
+                                            FinArgs fa, const FoldCall& fc, float* sm) {
     EEG_DIMS_NT(g, NTB);
     TRACE(g, 1, TR_ENTRY);
     unsigned dk0;
@@ -836,7 +825,6 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
     constexpr bool VPF = TT != 0;
     float vpf[MO][8];
     if (VPF && b0 < b1) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
-    hook();                                        // (k_step: the coefficients of this step's BN1 / BN2)
 
     for (int i = tid; i < 3 * F2 * RS2; i += NTB) sm[i] = 0.f;     // pads stay zero
     for (int i = tid; i < F2MAX * (K2 + F2MAX); i += NTB) {
@@ -978,7 +966,7 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
             pub(row + ((k < 2 ? 0 : F2) + o), rv[0]);
         }
     }
-    if constexpr (!PERSIST) {
+    {
         double* dsm = (double*)sm;
         if (grid_reduce(g, part, g.nB, fa, dsm)) { fin2(g, dsm + 2, fa); TRACE(g, 1, TR_FIN); }
     }
@@ -994,8 +982,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
                                                       float* __restrict__ r3g, float* __restrict__ part,
                                                       FinArgs fa, FoldCall fc) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    pass_b_body<K1, CC, TT, FF, FOLD, false>(g, prm, coef, vg, mask2, d2g, E1g, E2g, q3g, r3g, part, fa, fc, sm,
-                                             NoHook{});
+    pass_b_body<K1, CC, TT, FF, FOLD>(g, prm, coef, vg, mask2, d2g, E1g, E2g, q3g, r3g, part, fa, fc, sm);
 }
 
 // ================================================================================================
@@ -1007,22 +994,19 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 // Per trial: x DMA (for this trial's dws GEMM) | dy2 from v -> dy rows | lag correlation (dy, s) and
 // FIR^T (dy -> e, in place) | barrier | next trial's s / dp2 DMA and v loads | dws GEMM (e, x) | barrier
 // ================================================================================================
-// PERSIST: `hook` (k_step's wait for pass D's reduction and its finalize) runs after the first trial's
-// s / dp2 DMA and v loads are issued, with the dy / x rows (not yet written) as its LDS scratch
 // EEGNET_LDSX_E = n (counter builds only, wrong results): drop one class of pass E's LDS accesses to
 // read its share of SQ_LDS_BANK_CONFLICT (tools/lds_probe.sh): 1 dp2 reads, 2 FIR^T windows, 3 lag
 // correlation operands, 4 dws GEMM operands, 5 dy stores, 6 e stores, 7 the in-loop LDS-DMAs
 #ifndef EEGNET_LDSX_E
 #define EEGNET_LDSX_E 0
 #endif
-template <int K1, int CC, int TT, int FF, bool FOLD, bool PERSIST, class Hook>
+template <int K1, int CC, int TT, int FF, bool FOLD>
 __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   // Adam (finalize) writes it
                                             const float* coef,    // the finalize writes it: no __restrict__
                                             const float* __restrict__ x,
                                             const float* __restrict__ sg, const float* __restrict__ vg,
                                             const float* __restrict__ dp2g,
-                                            float* __restrict__ part, FinArgs fa, const FoldCall& fc, float* sm,
-                                            const Hook& hook) {
+                                            float* __restrict__ part, FinArgs fa, const FoldCall& fc, float* sm) {
     using G_ = KG<K1>;
     EEG_DIMS_NT(g, NTB);
     const int XP = EEG_XP(TT, g);
@@ -1155,7 +1139,6 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
         if constexpr (VPF) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
         TRACE_PS(g, 4);
     }
-    hook();                                        // (k_step: scratch = the dy / x rows, not yet written)
     if constexpr (XDMA) zero_pads(sm, 2 * F2 + C, RS, LP, T, tid);   // the data windows are DMA'd / written
     load_taps<K1, NTS>(g, prm, D, F2, wave, tap);
     TRACE_PS(g, 2);
@@ -1175,8 +1158,8 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
         }
         if (lane < 8 * RPW && RPW * wave + (lane >> 3) < F2) CT[8 * RPW * wave + lane] = cv;
     }
-    if constexpr (!PERSIST) adam_scalars_publish(g, fa);
-    const int step0 = PERSIST ? 0 : adam_step0(g, fa);   // before the reduction ticket (adam_slice)
+    adam_scalars_publish(g, fa);
+    const int step0 = adam_step0(g, fa);   // before the reduction ticket (adam_slice)
     if constexpr (XDMA) barrier_vm<0>();          // first s / dp2 landed (asm DMA), pads and tables written
     else __syncthreads();
     if constexpr (!XDMA) {
@@ -1567,7 +1550,7 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
         for (int w = ct2 * wpc; w < (ct2 + 1) * wpc; ++w) a += red[w * 256 + oo2 * 16 + cc];
         pub(row + (QR * K1 + p), a);
     }
-    if constexpr (!PERSIST) {
+    {
         double* dsm = (double*)sm;
         // fin5's inputs, loaded before the ticket by every workgroup (the winner's are in hand when it
         // starts fin5; eegnet_finalize.hip Fin5Stage).  Not for a deferred (synchronised-BN) pass: its
@@ -1591,7 +1574,7 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_e(Geo g, const float* prm,  
                                                       const float* __restrict__ dp2g,
                                                       float* __restrict__ part, FinArgs fa, FoldCall fc) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    pass_e_body<K1, CC, TT, FF, FOLD, false>(g, prm, coef, x, sg, vg, dp2g, part, fa, fc, sm, NoHook{});
+    pass_e_body<K1, CC, TT, FF, FOLD>(g, prm, coef, x, sg, vg, dp2g, part, fa, fc, sm);
 }
 
 }  // namespace eeg

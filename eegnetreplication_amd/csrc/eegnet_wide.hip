@@ -1033,12 +1033,14 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
     constexpr int NPD = 4;                             // float4 per thread and plane at cfg5
     floatx4 pd[PFD ? 3 : 1][PFD ? NPD : 1], pe1[PFD ? NPD : 1], pe2[PFD ? NPD : 1];
     auto planes_load = [&](int bb) {
-        const floatx4* s0 = reinterpret_cast<const floatx4*>(d2g + (size_t)bb * F2 * T1);
-        const floatx4* s1 = reinterpret_cast<const floatx4*>(q3g + (size_t)bb * F2 * T1);
-        const floatx4* s2 = reinterpret_cast<const floatx4*>(r3g + (size_t)bb * F2 * T1);
+        if constexpr (PFD) {               // (the only caller; keeps the 1 x 1 arrays of !PFD unindexed)
+            const floatx4* s0 = reinterpret_cast<const floatx4*>(d2g + (size_t)bb * F2 * T1);
+            const floatx4* s1 = reinterpret_cast<const floatx4*>(q3g + (size_t)bb * F2 * T1);
+            const floatx4* s2 = reinterpret_cast<const floatx4*>(r3g + (size_t)bb * F2 * T1);
 #pragma unroll
-        for (int j = 0; j < NPD; ++j) {
-            pd[0][j] = s0[tid + NT * j]; pd[1][j] = s1[tid + NT * j]; pd[2][j] = s2[tid + NT * j];
+            for (int j = 0; j < NPD; ++j) {
+                pd[0][j] = s0[tid + NT * j]; pd[1][j] = s1[tid + NT * j]; pd[2][j] = s2[tid + NT * j];
+            }
         }
     };
     if constexpr (PFD)

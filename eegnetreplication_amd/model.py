@@ -331,17 +331,10 @@ class FusedAdamState:
 
 
 class FusedTrainer:
-    """Whole hot-loop iteration (model.py:141-148) as one device sequence per batch.
+    """Whole hot-loop iteration (model.py:141-148) as one device sequence per batch."""
 
-    ``persist``: run each step as ONE launch of a co-resident grid (EEGNET_PERSIST, csrc/eegnet_persist.hip;
-    the 22 x 256 / 257 EEGNet-8,2 shapes, others take the five-launch step).  Off by default: measured
-    slower than the five launches (0.270 against 0.241 ms per B = 4096 step).  Its
-    workgroups wait for each other at the BatchNorm reductions, so two such steps must not run on one
-    device at once (steps on one stream are ordered)."""
-
-    def __init__(self, model: EEGNet, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, optimizer=None, persist=False):
+    def __init__(self, model: EEGNet, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, optimizer=None):
         self.model = model
-        self.persist = bool(persist)
         self.lr, self.betas, self.eps = lr, betas, eps
         self.adam = FusedAdamState(model, optimizer)
         dev = model.flat_parameters().device
@@ -361,7 +354,7 @@ class FusedTrainer:
         ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
                        self.adam.grads, self.adam.state, self.adam.step, self.workspace(x.shape[0]),
                        self.loss, logits=logits, lr=self.lr, betas=self.betas, eps=self.eps,
-                       nbt=m.flat_num_batches_tracked(), persist=self.persist)
+                       nbt=m.flat_num_batches_tracked())
         return self.loss
 
 

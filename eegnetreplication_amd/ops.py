@@ -121,7 +121,6 @@ def forward_train(shape: Shape, flat_params, bn_flat, x, ws, seed: int, offset: 
 
 NO_CLAMP = 1
 KEY_FROM_STEP = 2      # include/eegnet_abi.h: dropout key follows the device Adam step (graphs)
-PERSIST = 4            # include/eegnet_abi.h: the step as one launch of a co-resident grid (k_step)
 
 
 def backward(shape: Shape, flat_params, x, ws, seed: int, offset: int, dlogits=None, labels=None,
@@ -204,18 +203,16 @@ def pad_x_rows(x: torch.Tensor, pitch: int) -> torch.Tensor:
 
 def train_step(shape: Shape, flat_params, bn_flat, x, labels, seed: int, offset: int, grads,
                adam_state, step_i32, ws, loss, logits=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-7,
-               p: float | None = None, clamp=True, nbt=None, key_from_step=False, persist=False):
+               p: float | None = None, clamp=True, nbt=None, key_from_step=False):
     """One fused hot-loop iteration (model.py:141-148) on the device, no host sync.
-    ``adam_state=None`` stops after the gradients (data-parallel).  ``persist``: EEGNET_PERSIST -- one
-    launch whose workgroups wait for each other; the caller guarantees no other persistent step runs
-    on the device at the same time (another stream or process)."""
+    ``adam_state=None`` stops after the gradients (data-parallel)."""
     d = shape.dims(x.shape[0], p, x_pitch_of(x))
     _lib.check(_lib.load().eegnet_train_step(
         ctypes.byref(d), _ptr(flat_params), _ptr(bn_flat), _ptr(x), _ptr(labels),
         ctypes.c_uint64(seed), ctypes.c_uint64(offset), _ptr(grads), _ptr(adam_state),
         _ptr(step_i32), ctypes.c_float(lr), ctypes.c_float(betas[0]), ctypes.c_float(betas[1]),
         ctypes.c_float(eps), _ptr(loss), _ptr(logits), _ptr(ws), _stream(),
-        (0 if clamp else NO_CLAMP) | (KEY_FROM_STEP if key_from_step else 0) | (PERSIST if persist else 0),
+        (0 if clamp else NO_CLAMP) | (KEY_FROM_STEP if key_from_step else 0),
         _ptr(nbt)), "eegnet_train_step")
 
 

@@ -66,12 +66,10 @@ enum { EEGNET_TRAIN = 1, EEGNET_EVAL = 0 };
 /* eegnet_backward flags */
 enum {
     EEGNET_NO_CLAMP = 1,      /* leave model.py:44/84 clamps to eegnet_clamp_grads (after an all-reduce) */
-    EEGNET_KEY_FROM_STEP = 2, /* eegnet_train_step: dropout key = mix(seed, offset + *step), read on the
+    EEGNET_KEY_FROM_STEP = 2  /* eegnet_train_step: dropout key = mix(seed, offset + *step), read on the
                                  device, so a captured hipGraph draws fresh masks on every replay */
-    EEGNET_PERSIST = 4        /* eegnet_train_step: run the step as ONE launch of a co-resident grid (the
-                                 22 x 256 / 257 EEGNet-8,2 shapes; other shapes ignore it).  Its workgroups
-                                 wait for each other, so the caller must not run another EEGNET_PERSIST
-                                 step on the device concurrently (another stream) */
+    /* 4 (round 5's opt-in one-launch persistent step) is retired: eegnet_train_step rejects any other
+       bit with EEGNET_EINVAL */
 };
 
 /* Number of fp32 elements of the flat parameter buffer for these dims. */
@@ -204,7 +202,7 @@ int eegnet_x_stats(const eegnet_dims* dims, int64_t n, const float* x, float* ou
 /* Optional per-kernel device timing for benchmarks: `on` is a bitmask of kernel ids (bit i = the
  * i-th name eegnet_profile_collect reports: k_pass_a, k_pass_b, k_pass_c, k_pass_d, k_pass_e,
  * k_adam, k_infer, memset_tickets, k_infer_bf16, k_wpass_a, k_wpass_b, k_wpass_b2, k_wpass_c,
- * k_wpass_d, k_wpass_e, k_winfer, k_coltail, k_xstats, k_step; -1 = all, 0 = off; the k_w* kernels are the F2 > 16 path).  Every selected kernel this
+ * k_wpass_d, k_wpass_e, k_winfer, k_coltail, k_xstats; -1 = all, 0 = off; the k_w* kernels are the F2 > 16 path).  Every selected kernel this
  * thread launches through the calls above is bracketed by hipEvents.  eegnet_profile_collect
  * synchronises them and reports, per kernel name (32-byte slots in `names`), launch count and
  * summed device ms; it returns the number of kernels in *n_out.  Not for use under hipGraph

@@ -173,3 +173,29 @@ def test_x_stats_width_matches_pass_a_row_head():
         want = K1 + 1 + R * (R + 1) // 2 + P * (P + 1) // 2 + R + P
         assert lib.eegnet_x_stats_width(ctypes.byref(_lib.dims(64, 22, 257, K1=K1))) == want
     assert lib.eegnet_x_stats_width(ctypes.byref(_lib.dims(64, 64, 512, F1=16, D=4))) < 0    # narrow path only
+
+
+def test_retired_persist_flag_is_rejected():
+    """Round 5's opt-in one-launch persistent step (flag bit 4) is gone from the shipped library: the
+    C-ABI rejects that bit (and every other unknown one) before any launch, so no caller -- FusedTrainer,
+    DataParallelTrainer, FoldBatch or a C binding -- can reach a step whose results are not the
+    five-launch step's bit for bit.  Runs without a GPU: the flag check precedes every device call."""
+    import ctypes
+    import inspect
+    from eegnetreplication_amd import _lib, ops
+    from eegnetreplication_amd.model import FusedTrainer
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libeegnet_hip.so not built")
+    assert "persist" not in inspect.signature(FusedTrainer).parameters
+    assert "persist" not in inspect.signature(ops.train_step).parameters
+    assert not hasattr(ops, "PERSIST")
+    lib = _lib.load()
+    d = _lib.dims(64, 22, 256)
+    dummy = ctypes.c_void_p(256)                     # never dereferenced: the call fails on the flags
+    for flags in (4, 4 | 2, 8, 1 << 20):
+        rc = lib.eegnet_train_step(ctypes.byref(d), dummy, dummy, dummy, dummy, 1, 2, dummy, dummy, dummy,
+                                   1e-3, 0.9, 0.999, 1e-7, dummy, None, dummy, None, flags, None)
+        assert rc == -1, flags
+        assert b"unknown flags" in lib.eegnet_last_error()
+    hdr = open(os.path.join(ROOT, "include", "eegnet_abi.h")).read()
+    assert "EEGNET_PERSIST" not in hdr

@@ -125,3 +125,25 @@ def test_bf16_eval_rejects_bad_input():
     m.train()
     with pytest.raises(RuntimeError):
         m(torch.zeros(2, 22, 256, dtype=torch.bfloat16, device=dev))
+
+
+@pytest.mark.parametrize("C,T,F1,D,nwg", [(64, 512, 16, 4, 512), (22, 256, 8, 2, 256)])
+def test_bf16_eval_nonfinite_trial_stays_private(C, T, F1, D, nwg):
+    """A trial with non-finite input must not leak into the next trial a workgroup runs (in the
+    reference every trial's output is its own, model.py:91-99).  The cfg5 chunk kernel lays the block-2
+    tail's z image over the s rows whose pad positions the FIR reads with zero taps (0 * Inf = NaN),
+    so those pads are re-zeroed after every tail.  The first trial of every workgroup is
+    NaN / Inf; every later trial must come out finite and bit-identical to its run without them."""
+    dev = _dev()
+    m = _model(C, T, F1, D, seed=23).to(dev).eval()
+    B = 3 * nwg                                        # grid = nwg workgroups: three trials each
+    g = torch.Generator(device=dev).manual_seed(9)
+    x = torch.randn(B, C, T, device=dev, generator=g).to(torch.bfloat16)
+    x[:nwg // 2] = float("nan")
+    x[nwg // 2:nwg, :, T // 3] = float("inf")
+    with torch.no_grad():
+        full = m(x)
+        clean = m(x[nwg:].contiguous())
+    torch.cuda.synchronize()
+    assert torch.isfinite(full[nwg:]).all(), "a non-finite trial leaked into a later trial"
+    assert torch.equal(full[nwg:], clean), "later trials depend on the earlier trials of their workgroup"

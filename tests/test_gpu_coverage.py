@@ -222,46 +222,3 @@ def test_large_batch_against_float64():
             assert_close(b.cpu().numpy(), r, name=k)
 
 
-@pytest.mark.parametrize("Tt", [256, 257])
-def test_persistent_step_against_float64(Tt):
-    """The persistent step (k_step: the five passes as phases of one co-resident launch, per-workgroup
-    finalizes, distributed Adam; FusedTrainer(persist=True)) at cfg2's B = 4096 with the device dropout
-    generator: loss, all 12 gradients, the running statistics and the parameters after Adam against the
-    reference layer stack in float64 given the restated device masks, at rtol 1e-4."""
-    from oracle import torch_ref as tr
-    from eegnetreplication_amd import FusedTrainer
-    from hip_cases import device_masks
-    dev = _dev()
-    B, C, T = 4096, 22, Tt
-    m = random_model(C, T, p=0.5, seed=3, perturb_bn=False).to(dev).train()
-    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
-    x_np, y_np = make_inputs(B, C, T, 4321)
-    x, y = torch.from_numpy(x_np).to(dev), torch.from_numpy(y_np).to(dev)
-    seed, offset = 77, 5
-    m.next_dropout_key = lambda: (seed, offset)
-    trn = FusedTrainer(m, persist=True)
-    loss = float(trn.step(x, y))
-    torch.cuda.synchronize()
-    m2, m3 = device_masks(B, 16, T, seed, offset, 0.5)
-    ref = tr.TorchRefEEGNet(state, p=0.5, device=dev, dtype=torch.float64)
-    opt = torch.optim.Adam(ref.parameters(), lr=1e-3, eps=1e-7)
-    rl = ref(x.double(), (torch.from_numpy(m2).to(dev), torch.from_numpy(m3).to(dev)))
-    rloss = torch.nn.functional.cross_entropy(rl, y)
-    opt.zero_grad()
-    rloss.backward()
-    assert abs(loss - float(rloss)) <= 1e-4 * max(1.0, abs(float(rloss)))
-    n, gr = 0, {}
-    for k, p in m.named_parameters():
-        gr[k] = trn.adam.grads[n:n + p.numel()].view(p.shape).cpu().numpy()
-        n += p.numel()
-    assert_grads_close(gr, {k: ref.params[k].grad.cpu().numpy() for k in PARAM_NAMES}, prefix="k_step grad.")
-    for k, b in m.named_buffers():
-        r = ref.buffers[k].cpu().numpy()
-        if "running_mean" in k:
-            assert_close(b.cpu().numpy(), r, atol_abs=1e-6, name=k)
-        elif "running_var" in k:
-            assert_close(b.cpu().numpy(), r, name=k)
-    opt.step()
-    from golden_util import assert_params_close
-    assert_params_close({k: p.detach().cpu().numpy() for k, p in m.named_parameters()},
-                        {k: ref.params[k].detach().cpu().numpy() for k in PARAM_NAMES}, prefix="k_step step1.")
