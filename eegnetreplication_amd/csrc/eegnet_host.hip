@@ -70,6 +70,13 @@ static void b2_lds(Geo* g, int nw) {
 #endif
 static bool use_b2_narrow(const Geo&) { return EEGNET_B2 == 1; }
 
+// Pass D of the F2 <= 16 step: the row-layout kernel k_pass_dr (two 512-thread workgroups per CU on the
+// streaming grid, the workgroup on one trial at a time; eegnet_passes.hip), or -DEEGNET_D1=1 the
+// one-trial-per-wave k_pass_d of rounds 1-5 (A/B builds)
+#ifndef EEGNET_D1
+#define EEGNET_D1 0
+#endif
+
 // workgroups per CU slot of the streaming passes A / B / E (-DEEGNET_GRIDS_MULT=n, experiments): with
 // more workgroups than resident slots the dispatcher refills a CU's early-finishing slot, so the two
 // resident workgroups' skew turns into load balance; the same for passes C / D (-DEEGNET_GRIDC_MULT)
@@ -157,7 +164,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->nwC = std::max(1, std::min(spec ? NWAVE : NTHS / 64, (LDS_MAX / 4) / pwC));
     g->nwD = std::max(1, std::min(NTHS / 64, (LDS_MAX / 4) / pwD));
     g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);
-    g->ldsD = std::max(g->nwD * pwD, g->nwD * g->nD);
+    g->ldsD = EEGNET_D1 ? std::max(g->nwD * pwD, g->nwD * g->nD)
+                        : std::max(dr_lds_floats(spec ? 1 : MAXT1Q), dr_tail_floats(spec));
     g->ldsE = std::max((2 * g->F2 + g->C) * g->RS + rup(g->F2 * g->T1, 4) + 8 * g->F2,
                        NWB * 256 * (1 + (15 + g->K1 - 1) / 16 + 1));   // after the loop: dws, Cq tiles
     g->ldsI = rows1 + g->F2 * g->RS + 2 * g->F2 * g->RS2 + nf4;
@@ -246,7 +254,7 @@ static WsLayout make_layout(const Geo& g) {
     L.partA = take((size_t)g.gridS * g.nA * 4);
     L.partB = take((size_t)std::max(g.gridS, g.grid) * g.nB * 4);
     L.partC = take((size_t)std::max(g.grid, g.gridB2) * g.nC * 4);
-    L.partD = take((size_t)std::max(g.grid, g.gridB2) * g.nD * 4);
+    L.partD = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridS) * g.nD * 4);   // (k_pass_dr: gridS)
     L.partE = take((size_t)g.gridS * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
     L.sums = take((size_t)nmax * 8 * NGRPMAX);
@@ -326,7 +334,9 @@ static void set_attrs_shape() {
                           (const void*)k_pass_b<K1, CC, TT, FF, true>, (const void*)k_pass_c<K1, CC, TT, FF, true>,
                           (const void*)k_pass_e<K1, CC, TT, FF, true>,
                           (const void*)k_pass_d<K1, CC, TT, FF, false, false>,
-                          (const void*)k_pass_d<K1, CC, TT, FF, true, false>})
+                          (const void*)k_pass_d<K1, CC, TT, FF, true, false>,
+                          (const void*)k_pass_dr<K1, CC, TT, FF>, (const void*)k_pass_dr<K1, CC, TT, FF, false, false>,
+                          (const void*)k_pass_dr<K1, CC, TT, FF, true, false>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipFuncSetAttribute((const void*)k_infer<K1, CC, TT, FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
@@ -546,6 +556,21 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     } else {
     if (only < 0 || only == 2) { { PROF(KID_C); EEG_DISPATCH(K1, g, LAUNCH_CB);
     } LAUNCH_CHECK("k_pass_c(bwd)"); }
+#define LAUNCH_DR(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_dr<K, CC, TT, FF, true, false>), dim3(g.gridS, nf), dim3(NTB), g.ldsD * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
+                       (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
+                       m2, m3, dl, (float*)(ws + L.dp2), \
+                       (float*)(ws + L.partD), fd, fc); \
+    else if (m2 || m3) hipLaunchKernelGGL((k_pass_dr<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsD * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
+                       (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
+                       m2, m3, dl, (float*)(ws + L.dp2), \
+                       (float*)(ws + L.partD), fd, fc); \
+    else hipLaunchKernelGGL((k_pass_dr<K, CC, TT, FF, false, false>), dim3(g.gridS, nf), dim3(NTB), g.ldsD * 4, s, \
+                       g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
+                       (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
+                       m2, m3, dl, (float*)(ws + L.dp2), \
+                       (float*)(ws + L.partD), fd, fc)
 #define LAUNCH_D(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_d<K, CC, TT, FF, true, false>), dim3(g.grid, nf), dim3(64 * g.nwD), g.ldsD * 4, s, \
                        g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), \
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
@@ -561,7 +586,7 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
                        m2, m3, dl, (float*)(ws + L.dp2), \
                        (float*)(ws + L.partD), fd, fc)
-    if (only < 0 || only == 3) { { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_D);
+    if (only < 0 || only == 3) { { PROF(KID_D); if (EEGNET_D1) EEG_DISPATCH(K1, g, LAUNCH_D); else EEG_DISPATCH(K1, g, LAUNCH_DR);
     } LAUNCH_CHECK("k_pass_d"); }
     }
 #define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \

@@ -109,6 +109,26 @@ __device__ __forceinline__ void conv16_same_t(const float (&x)[MQ], const float*
     }
 }
 
+// the same as two independent chains (taps 0-7 over left shifts, 8-15 over right shifts) added at
+// the end: half the dependent-latency chain per row
+template <int MQ>
+__device__ __forceinline__ void conv16_same_t2(const float (&x)[MQ], const float* __restrict__ w, float (&y)[MQ],
+                                               int lane) {
+    float s[MQ], u[MQ], y1[MQ];
+#pragma unroll
+    for (int m = 0; m < MQ; ++m) { y[m] = w[7] * x[m]; s[m] = x[m]; u[m] = x[m]; y1[m] = 0.f; }
+#pragma unroll
+    for (int k = 6; k >= 0; --k) {
+        shl1<MQ>(s, lane);                         // s = x[t + 7 - k]
+        shr1<MQ>(u, lane);                         // u = x[t - (14 - k - 7)] for tap 14 - k
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) { y[m] = fmaf(w[k], s[m], y[m]); y1[m] = fmaf(w[14 - k], u[m], y1[m]); }
+    }
+    shr1<MQ>(u, lane);                             // tap 15: x[t - 8]
+#pragma unroll
+    for (int m = 0; m < MQ; ++m) y[m] += fmaf(w[15], u[m], y1[m]);
+}
+
 // d2 rows of trial b into registers (lane t, chunk m); zero beyond T1.  Wave-uniform row base:
 // saddr + 32-bit lane offset loads.
 template <int MQ>
@@ -618,6 +638,418 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
     __syncthreads();
     float* row = part + (size_t)blockIdx.x * g.nD;
     for (int c = tid; c < g.nD; c += blockDim.x) pub(row + c, wave_rows_sum<NTHS / 64>(red, nw, g.nD, c));
+    double* dsm = (double*)sm;
+    if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
+}
+
+// ================================================================================================
+// Pass D in the streaming passes' row layout (k_pass_dr, the default; k_pass_d above is the
+// -DEEGNET_D1=1 build).  k_pass_d gives each wave a whole trial, so one trial is a ~12 us serial chain
+// of one wave at two waves per SIMD (225 VGPRs): scalar weight loads chained row after row, the
+// pointwise mix over 16 rows in one lane, and 16 conv rows back to back.  Here the workgroup works on
+// one trial at a time like passes B and E: wave w owns rows o = 2w, 2w + 1 of the trial's [F2, T1]
+// planes, lane t owns pooled sample t (+ 64 m), two 512-thread workgroups per CU.
+//   step 1 (row-local): BN3 backward of the own rows -> dr rows and the q rows into LDS (alternate
+//     buffers per trial, so one barrier per trial)
+//   barrier
+//   step 2: dW3 += dr q^T (MFMA, the T1 k-steps dealt over the waves), dq = W3^T dr for the own rows
+//     (all dr rows from LDS), dw2 (own rows, lane-shifted d2), dd2 = the transposed 1x16 conv (lane
+//     shifts), dropout -> dp2, BN2-backward sums
+// The trial's five plane rows per lane and its dlogits come a trial ahead (registers / SGPRs); the
+// block-2 weights sit in LDS and reach the SGPRs by readfirstlane.
+// part row: [dW3 F2*F2][dw2 F2*16][Sdz2 F2][Sdz2x F2] (k_pass_d's, finalize 4 unchanged)
+// LDS: dr rows x 2 | q rows x 2 (F2MAX rows of RSD floats) | W3^T [F2MAX][F2MAX] | w2 [F2MAX][16]
+// ================================================================================================
+// row stride 64 MQ + 2: a 32-lane group of the MFMA operand reads (16 rows x 2 consecutive k) covers
+// banks 2 li + lk -- 32 distinct banks (ds_read_b32 banks mod 32 per 32-lane group)
+__host__ __device__ constexpr int dr_stride(int MQ) { return 64 * MQ + 2; }
+__host__ __device__ constexpr int dr_lds_floats(int MQ) { return 4 * F2MAX * dr_stride(MQ) + F2MAX * (F2MAX + K2); }
+// after the loop: dW3 tiles [NWB][256], the owned row [18 F2MAX], and (T1 = 64) the Hankel tiles
+__host__ __device__ constexpr int dr_tail_floats(bool hankel) { return NWB * 256 + 18 * F2MAX + (hankel ? NWB * RPW * 2 * 256 : 0); }
+
+__device__ __forceinline__ float sgpr_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+template <int K1, int CC, int TT, int FF, bool FOLD = false, bool MASK = true>
+__global__ __launch_bounds__(NTB, TT ? WPEB : 2) void k_pass_dr(Geo g, const float* __restrict__ prm,
+                                                  const float* coef,    // the finalize writes it: no __restrict__
+                                                  const float* __restrict__ d2g,
+                                                  const float* __restrict__ E1g,
+                                                  const float* __restrict__ E2g,
+                                                  const float* __restrict__ q3g,
+                                                  const float* __restrict__ r3g,
+                                                  const uint8_t* __restrict__ mask2,
+                                                  const uint8_t* __restrict__ mask3,
+                                                  const float* __restrict__ dl,
+                                                  float* __restrict__ dp2g, float* __restrict__ part,
+                                                  FinArgs fa, FoldCall fc) {
+    EEG_DIMS_NT(g, NTB);
+    TRACE(g, 3, TR_ENTRY);
+    unsigned dk0, dk1;
+    if (FOLD) {
+        const eegnet_fold f = fold_rec(fc);
+        char* ws = (char*)f.ws;
+        prm = f.params;
+        coef = (const float*)(ws + fc.off.coef);
+        d2g = (const float*)(ws + fc.off.d2);
+        E1g = (const float*)(ws + fc.off.E1); E2g = (const float*)(ws + fc.off.E2);
+        q3g = (const float*)(ws + fc.off.q3); r3g = (const float*)(ws + fc.off.r3);
+        mask2 = nullptr; mask3 = nullptr;
+        dl = (const float*)(ws + fc.off.dl);
+        dp2g = (float*)(ws + fc.off.dp2);
+        part = (float*)(ws + fc.off.partD);
+        fa = fold_fin(fc, f, TK_D, 0, 0, false, false, g.nparam);
+        dk0 = fold_drop_key(fc, f, 0);
+        dk1 = fold_drop_key(fc, f, 1);
+    } else {
+        dk0 = drop_key(g, 0);
+        dk1 = drop_key(g, 1);
+    }
+    if constexpr (!MASK) { mask2 = nullptr; mask3 = nullptr; }
+    constexpr int MQ = TT ? (TT / 4 + 63) / 64 : MAXT1Q;
+    constexpr int RSD = dr_stride(MQ);
+    constexpr int NKS = TT ? (TT / 4 + 3) / 4 : 16 * MAXT1Q;    // MFMA k-steps bound (rows are zero past T1)
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* const DR0 = sm;                              // [2][F2MAX][RSD]
+    float* const Q0 = DR0 + 2 * F2MAX * RSD;            // [2][F2MAX][RSD]
+    float* const W3t = Q0 + 2 * F2MAX * RSD;            // W3t[i][j] = W3[j][i]
+    float* const W2t = W3t + F2MAX * F2MAX;             // w2[o][k]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int li = lane & 15, lk = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int b0, b1;
+    trial_range(g, b0, b1);
+    const int nks = TT ? NKS : (T1 + 3) >> 2;
+    // the compile-time shapes fill every row and lane (F2 = 16 rows, T1 = 64 samples): no guards, so no
+    // branches around loads -- a branch makes the waitcnt pass wait for every load in flight (vmcnt(0))
+    // at the loop top, which turned the prefetch into a stall
+    constexpr bool FULL = TT && FF == F2MAX && TT / 4 == 64 * MQ;
+
+    // plane rows of a trial in two register slots (rows RPW w + r, lanes t = lane + 64 m; zero past
+    // T1 / F2).  The loop runs the trials in pairs, slot 0 then slot 1, and a slot is reloaded with
+    // the trial two ahead as soon as its rows have been read (r, q and dlogits after step 1; d2, E1, E2
+    // after step 2): no register copies, so a load is never waited for before its own trial (copies
+    // of freshly loaded registers had made the waitcnt pass wait for the newest loads every trial).
+    // An odd trial range ends with a ghost trial: the last trial again, its sums gated off (its dp2
+    // stores repeat the same values).
+    float sr[2][RPW][MQ], sq[2][RPW][MQ], sd[2][RPW][MQ], se1[2][RPW][MQ], se2[2][RPW][MQ];
+    floatx4 sdl[2];
+    // a row's wave-uniform base (scalar) and the lane's 32-bit offset: saddr-form loads, no 64-bit
+    // address VGPRs
+    auto row_base = [&](int bb, int r) {
+        const int o = RPW * wave + r;
+        return (size_t)bb * F2 * T1 + (size_t)((FULL || o < F2) ? o * T1 : 0);
+    };
+    auto lane_off = [&](int r, int m, bool& ok) {
+        const int o = RPW * wave + r, t = lane + 64 * m;
+        ok = FULL || (o < F2 && t < T1);
+        return ok ? t : 0;
+    };
+    auto load_rq = [&](int bb, float (&xr)[RPW][MQ], float (&xq)[RPW][MQ], floatx4& xdl) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) {
+                bool ok;
+                const int i = lane_off(r, m, ok);
+                const size_t rb_ = row_base(bb, r);
+                const float vr = (r3g + rb_)[i], vq = (q3g + rb_)[i];
+                xr[r][m] = ok ? vr : 0.f;
+                xq[r][m] = ok ? vq : 0.f;
+            }
+        xdl = ldc(reinterpret_cast<const floatx4*>(dl) + bb);
+    };
+    auto load_de = [&](int bb, float (&xd)[RPW][MQ], float (&x1)[RPW][MQ], float (&x2)[RPW][MQ]) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) {
+                bool ok;
+                const int i = lane_off(r, m, ok);
+                const size_t rb_ = row_base(bb, r);
+                const float vd = (d2g + rb_)[i], v1 = (E1g + rb_)[i], v2 = (E2g + rb_)[i];
+                xd[r][m] = ok ? vd : 0.f;
+                x1[r][m] = ok ? v1 : 0.f;
+                x2[r][m] = ok ? v2 : 0.f;
+            }
+    };
+
+    // weight tables; rows F2 .. F2MAX - 1 of the four row buffers stay zero (MFMA operand reads)
+    for (int i = tid; i < F2MAX * (F2MAX + K2); i += NTB) {
+        float v = 0.f;
+        if (i < F2MAX * F2MAX) {
+            const int ii = i / F2MAX, j = i - ii * F2MAX;
+            if (ii < F2 && j < F2) v = prm[g.o_W3 + j * F2 + ii];
+        } else {
+            const int k = i - F2MAX * F2MAX, o = k / K2;
+            if (o < F2) v = prm[g.o_w2 + k];
+        }
+        W3t[i] = v;
+    }
+    if (F2 < F2MAX)
+        for (int i = tid; i < 4 * (F2MAX - F2) * RSD; i += NTB) {
+            const int buf = i / ((F2MAX - F2) * RSD), k = i - buf * ((F2MAX - F2) * RSD);
+            DR0[buf * F2MAX * RSD + F2 * RSD + k] = 0.f;
+        }
+    // per-row BN3 constants (scalar loads: parameters and finalize 2 / 3's coefficients) and the
+    // classifier weights of the lane's pooled feature
+    float g3[RPW], b3[RPW], mu3[RPW], inv3[RPW], A3[RPW], B3[RPW], C3[RPW];
+    float wfl[RPW][MQ][NCLS];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int o = RPW * wave + r, oo = (FULL || o < F2) ? o : 0;
+        const bool on = FULL || o < F2;
+        g3[r] = on ? ldc(prm + g.o_g3 + oo) : 0.f;
+        b3[r] = on ? ldc(prm + g.o_b3 + oo) : 0.f;
+        mu3[r] = on ? ldc(coef + CF_MU3 * CSTR + oo) : 0.f;
+        inv3[r] = on ? ldc(coef + CF_INV3 * CSTR + oo) : 0.f;
+        A3[r] = on ? ldc(coef + CF_A3 * CSTR + oo) : 0.f;
+        B3[r] = on ? ldc(coef + CF_B3 * CSTR + oo) : 0.f;
+        C3[r] = on ? ldc(coef + CF_C3 * CSTR + oo) : 0.f;
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) {
+            const int t = lane + 64 * m;
+            const bool ft = on && t < 8 * T2;
+#pragma unroll
+            for (int n = 0; n < NCLS; ++n) wfl[r][m][n] = ft ? prm[g.o_Wfc + n * NF + oo * T2 + (t >> 3)] : 0.f;
+        }
+    }
+    floatx4 acc3 = {0.f, 0.f, 0.f, 0.f};        // dW3 tile: D[j = 4 lk + r][i = li]
+    // dw2 of the own rows.  FULL (T1 = 64): as pass E's lag correlation, a Hankel block product on the
+    // matrix cores -- t = 16 a + u, Cq[u][w] = sum_a dq[16 a + u] d2p[16 a + w - 7] (two 16 x 16 tiles,
+    // w < 32, K = the 4 blocks a), accumulated over the trials; dw2[k] = sum_u Cq[u][u + k] once, after
+    // the loop.  The A operand is the lane's own dq, the B operand its d2 row shifted by 7 / -9 lanes
+    // (ds_bpermute).  Other shapes: per-lane partials over lane-shifted d2 rows.
+    floatx4 hq[RPW][2];
+    float acc2[RPW][K2];
+    float sz1[RPW], sz2[RPW];                   // BN2-backward sums of the own rows
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        sz1[r] = 0.f; sz2[r] = 0.f;
+        hq[r][0] = acc3; hq[r][1] = acc3;
+#pragma unroll
+        for (int k = 0; k < K2; ++k) acc2[r][k] = 0.f;
+    }
+    // the first two trials' rows: issued after the table / weight loads, so the LDS stores above wait
+    // for those alone (trials past the range load the last trial's rows: unconditional loads)
+    const int blast = b1 > b0 ? b1 - 1 : b0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        load_rq(min(b0 + k, blast), sr[k], sq[k], sdl[k]);
+        load_de(min(b0 + k, blast), sd[k], se1[k], se2[k]);
+    }
+    barrier_lds();                           // tables and zero rows written (the row loads stay in flight)
+
+    TRACE(g, 3, TR_PRO);
+    TRACE_DECL();
+    auto trial = [&](const int bt, const bool live, const int buf, float (&xr)[RPW][MQ], float (&xq)[RPW][MQ],
+                     float (&xd)[RPW][MQ], float (&x1)[RPW][MQ], float (&x2)[RPW][MQ], floatx4& xdl) {
+        const int b = min(bt, blast), bn = min(bt + 2, blast);
+        float* DR = DR0 + buf * F2MAX * RSD;
+        float* Qb = Q0 + buf * F2MAX * RSD;
+        TRACE_PH(g, 3, 0, tph_);
+        // step 1: dh -> dropout -> dp3 -> dz3 = dp3/8 ELU'(z3) -> dr = A3 dz3 + B3 + C3 xh3 (finalize 3's
+        // batch constants), own rows; q rows alongside (the dW3 B operand)
+        const floatx4 dlv = xdl;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int o = RPW * wave + r;
+            if (FULL || o < F2) {
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) {
+                    const int t = lane + 64 * m;
+                    const float xh = (xr[r][m] - mu3[r]) * inv3[r];
+                    float dd = 0.f;
+#pragma unroll
+                    for (int n = 0; n < NCLS; ++n) dd = fmaf(dlv[n], wfl[r][m][n], dd);
+                    const bool ft = t < 8 * T2;
+                    const float kp = keep_mul(g, mask3, dk1, (unsigned)(b * NF + (ft ? o * T2 + (t >> 3) : 0)));
+                    const float dz = ft ? dd * kp * 0.125f * elu_d(fmaf(g3[r], xh, b3[r])) : 0.f;
+                    DR[o * RSD + t] = (FULL || t < T1) ? fmaf(A3[r], dz, fmaf(C3[r], xh, B3[r])) : 0.f;
+                    Qb[o * RSD + t] = xq[r][m];
+                }
+            }
+        }
+        load_rq(bn, xr, xq, xdl);
+        TRACE_PH(g, 3, 1, tph_);
+        // the trial's dr / q rows complete; the other buffers are rewritten only after every wave has
+        // passed the next trial's barrier (LDS only: the row loads stay in flight)
+        barrier_lds();
+        TRACE_PH(g, 3, 2, tph_);
+        // dW3[j][i] += sum_t dr[j][t] q[i][t] on the matrix cores: k-steps dealt over the waves
+        for (int ks = wave; ks < nks; ks += NWB) {
+            const float a = DR[li * RSD + 4 * ks + lk], bq = Qb[li * RSD + 4 * ks + lk];
+            acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(live ? a : 0.f, bq, acc3, 0, 0, 0);
+        }
+        // dq[i][t] = sum_j W3[j][i] dr[j][t] for the own rows i
+        float dq[RPW][MQ];
+        {
+            float dv[F2MAX][MQ];
+#pragma unroll
+            for (int j = 0; j < F2MAX; ++j)
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) dv[j][m] = j < F2 ? DR[j * RSD + lane + 64 * m] : 0.f;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int o = RPW * wave + r, oo = (FULL || o < F2) ? o : 0;
+                float w3r[F2MAX];
+#pragma unroll
+                for (int q4 = 0; q4 < F2MAX / 4; ++q4) {
+                    const floatx4 w = lds_ld4(W3t + oo * F2MAX + 4 * q4);
+                    w3r[4 * q4] = sgpr_f(w[0]); w3r[4 * q4 + 1] = sgpr_f(w[1]);
+                    w3r[4 * q4 + 2] = sgpr_f(w[2]); w3r[4 * q4 + 3] = sgpr_f(w[3]);
+                }
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int j = 0; j < F2MAX; ++j)
+                        if (j < F2) a = fmaf(w3r[j], dv[j][m], a);
+                    dq[r][m] = a;
+                }
+            }
+        }
+        TRACE_PH(g, 3, 3, tph_);
+        const size_t rb = (size_t)b * F2 * T1;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int o = RPW * wave + r;
+            if (!FULL && o >= F2) continue;
+            // dw2[o][k] += sum_t dq[o][t] d2p[o][t + k - 7]
+            if constexpr (FULL) {
+                const float dqg = live ? dq[r][0] : 0.f;
+                const int i0 = lane - 7, i1 = lane + 9;
+                const float d0 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(max(i0, 0) * 4, __builtin_bit_cast(int, xd[r][0])));
+                const float d1 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(min(i1, 63) * 4, __builtin_bit_cast(int, xd[r][0])));
+                hq[r][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(dqg, i0 >= 0 ? d0 : 0.f, hq[r][0], 0, 0, 0);
+                hq[r][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(dqg, i1 < 64 ? d1 : 0.f, hq[r][1], 0, 0, 0);
+            } else {
+                float s[MQ], dqg[MQ];
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) {
+                    dqg[m] = live ? dq[r][m] : 0.f;
+                    s[m] = xd[r][m];
+                    acc2[r][7] = fmaf(dqg[m], s[m], acc2[r][7]);
+                }
+#pragma unroll
+                for (int k = 8; k < K2; ++k) {
+                    shl1<MQ>(s, lane);
+#pragma unroll
+                    for (int m = 0; m < MQ; ++m) acc2[r][k] = fmaf(dqg[m], s[m], acc2[r][k]);
+                }
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) s[m] = xd[r][m];
+#pragma unroll
+                for (int k = 6; k >= 0; --k) {
+                    shr1<MQ>(s, lane);
+#pragma unroll
+                    for (int m = 0; m < MQ; ++m) acc2[r][k] = fmaf(dqg[m], s[m], acc2[r][k]);
+                }
+            }
+            // dd2 = conv16_same_t(dq) -> dropout -> dp2; BN2-backward sums (E1 / E2 of pass B)
+            float w2r[K2];
+#pragma unroll
+            for (int q4 = 0; q4 < K2 / 4; ++q4) {
+                const floatx4 w = lds_ld4(W2t + o * K2 + 4 * q4);
+                w2r[4 * q4] = sgpr_f(w[0]); w2r[4 * q4 + 1] = sgpr_f(w[1]);
+                w2r[4 * q4 + 2] = sgpr_f(w[2]); w2r[4 * q4 + 3] = sgpr_f(w[3]);
+            }
+            float y[MQ];
+            conv16_same_t2<MQ>(dq[r], w2r, y, lane);
+#pragma unroll
+            for (int m = 0; m < MQ; ++m) {
+                const int t = lane + 64 * m;
+                if (FULL || t < T1) {
+                    const int gi = o * T1 + t;
+                    const float dp = y[m] * keep_mul(g, mask2, dk0, (unsigned)(rb + gi));
+                    __builtin_nontemporal_store(dp, dp2g + rb + gi);
+                    const float dpg = live ? dp * 0.25f : 0.f;
+                    sz1[r] = fmaf(dpg, x1[r][m], sz1[r]);
+                    sz2[r] = fmaf(dpg, x2[r][m], sz2[r]);
+                }
+            }
+        }
+        load_de(bn, xd, x1, x2);
+        TRACE_PH(g, 3, 4, tph_);
+    };
+    for (int b = b0; b < b1; b += 2) {
+        pace_prio(b - b0, b1 - b0);
+        trial(b, true, 0, sr[0], sq[0], sd[0], se1[0], se2[0], sdl[0]);
+        trial(b + 1, b + 1 < b1, 1, sr[1], sq[1], sd[1], se1[1], se2[1], sdl[1]);
+    }
+    TRACE_LOOP(g, 3);
+    tail_prio();
+    // ---- workgroup reduction: dW3 tiles summed over the waves in wave order; dw2 / sums per owner ----
+    __syncthreads();                         // every wave is done with the row buffers
+    float* red = sm;                         // [NWB][256]
+    float* own = red + NWB * 256;            // [dw2 F2*16][Sdz2 F2][Sdz2x F2]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave * 256 + (4 * lk + r) * 16 + li] = acc3[r];
+    if constexpr (FULL) {
+        // dw2[k] = sum_u Cq[u][u + k] from the wave's Hankel tiles (its own LDS scratch)
+        float* hs = own + 18 * F2MAX + wave * (RPW * 2 * 256);
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) hs[((r * 2 + h) * 16 + 4 * lk + i) * 16 + li] = hq[r][h][i];
+        wave_lds_fence();
+        if (lane < RPW * K2) {
+            const int r = lane / K2, k = lane % K2;
+            float a = 0.f;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int w = u + k;
+                a += hs[((r * 2 + (w >> 4)) * 16 + u) * 16 + (w & 15)];
+            }
+            own[(RPW * wave + r) * K2 + k] = a;
+        }
+        float v[4] = {sz1[0], sz1[1], sz2[0], sz2[1]};
+        wave_reduce<4>(v);                   // lane 16 q: item q = (sz1, sz2)[q / 2] of row q % 2
+        if ((lane & 15) == 0) {
+            const int q = lane >> 4;
+            own[F2 * K2 + (q >> 1) * F2 + RPW * wave + (q & 1)] = v[0];
+        }
+    } else {
+        constexpr int NV = RPW * K2 + 2 * RPW;          // 36 items; lane 16 q holds item j + 9 q in v[j]
+        float v[NV];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+#pragma unroll
+            for (int k = 0; k < K2; ++k) v[r * K2 + k] = acc2[r][k];
+            v[RPW * K2 + r] = sz1[r];
+            v[RPW * K2 + RPW + r] = sz2[r];
+        }
+        wave_reduce<NV>(v);
+        if ((lane & 15) == 0) {
+            const int q = lane >> 4;
+#pragma unroll
+            for (int j = 0; j < NV / 4; ++j) {
+                const int item = j + (NV / 4) * q;
+                if (item < RPW * K2) {
+                    const int o = RPW * wave + item / K2;
+                    if (o < F2) own[o * K2 + item % K2] = v[j];
+                } else {
+                    const int e = item - RPW * K2, o = RPW * wave + (e % RPW);
+                    if (o < F2) own[F2 * K2 + (e / RPW) * F2 + o] = v[j];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    float* row = part + (size_t)blockIdx.x * g.nD;
+    for (int c = tid; c < g.nD; c += NTB) {
+        float val;
+        if (c < F2 * F2) {
+            const int j = c / F2, i = c - j * F2;
+            val = wave_rows_sum<NWB>(red, NWB, 256, j * 16 + i);
+        } else {
+            val = own[c - F2 * F2];
+        }
+        pub(row + c, val);
+    }
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
 }
