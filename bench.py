@@ -99,7 +99,7 @@ def kernel_algorithmic_wide(C=64, T=512, F1=16, D=4, K1=32):
 
 
 # waves per SIMD each kernel's launch configuration admits (workgroup size x workgroups per CU / 4 SIMDs)
-LAUNCH_WAVES_PER_SIMD = {"k_pass_a": 4, "k_pass_b": 4, "k_pass_c": 4, "k_pass_d": 2, "k_pass_e": 4,
+LAUNCH_WAVES_PER_SIMD = {"k_pass_a": 4, "k_pass_b": 4, "k_pass_c": 4, "k_pass_d": 4, "k_pass_dr": 4, "k_pass_e": 4,
                          "k_infer": 4, "k_wpass_a": 4, "k_wpass_b": 4, "k_wpass_b2": 2, "k_wpass_c": 2,
                          "k_wpass_d": 2, "k_wpass_e": 4, "k_infer_bf16_cfg5": 4}
 

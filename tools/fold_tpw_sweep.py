@@ -1,6 +1,6 @@
 """Real-protocol fold-launch throughput at a given EEGNET_FOLD_TPW (read once per process): the
 fused fold-indexed leg of bench.py's bench_folds only, at several fold-batch widths.
-    EEGNET_FOLD_TPW=13,32,6 python tools/fold_tpw_sweep.py 90 12"""
+    EEGNET_LIB=libeegnet_hip_t28.so python tools/fold_tpw_sweep.py 90 12   (a -DEEGNET_FOLD_TPW_S / _C build)"""
 import os
 import sys
 import time
@@ -31,7 +31,7 @@ def run(n_folds, n_train=1440, epochs=2, dev="cuda:0"):
 
 
 if __name__ == "__main__":
-    tpw = os.environ.get("EEGNET_FOLD_TPW", "default")
+    tpw = os.environ.get("EEGNET_LIB", "libeegnet_hip.so")
     for nf in [int(a) for a in sys.argv[1:]] or [90, 12]:
         print(f"tpw {tpw} folds {nf}: {run(nf, epochs=int(os.environ.get('EPOCHS', 2))) / 1e6:.3f} M trials/s",
               flush=True)
