@@ -161,9 +161,9 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     // passes C / D: one trial stream per wave, each with its own block-2 rows (row_stride_b2)
     g->RSW = row_stride_b2(g->T1);
     const int pwC = nf4, pwD = 3 * g->F2 * g->RSW + nf4;
-    g->nwC = std::max(1, std::min(spec ? NWAVE : NTHS / 64, (LDS_MAX / 4) / pwC));
+    g->nwC = std::max(1, std::min(spec ? NWAVE : NTHS / 64, (LDS_MAX / 4 - 4 * F2MAX) / pwC));
     g->nwD = std::max(1, std::min(NTHS / 64, (LDS_MAX / 4) / pwD));
-    g->ldsC = std::max(g->nwC * pwC, g->nwC * g->nC);
+    g->ldsC = std::max(g->nwC * pwC + 4 * F2MAX, g->nwC * g->nC);   // Hs rows + the BN3 constant table
     g->ldsD = EEGNET_D1 ? std::max(g->nwD * pwD, g->nwD * g->nD)
                         : std::max(dr_lds_floats(spec ? 1 : MAXT1Q), dr_tail_floats(spec));
     g->ldsE = std::max((2 * g->F2 + g->C) * g->RS + rup(g->F2 * g->T1, 4) + 8 * g->F2,

@@ -62,6 +62,11 @@ __device__ __forceinline__ float sum8_hi(float v) {
     return v;
 }
 
+// a wave-uniform value (e.g. from a uniform-address LDS read) moved to an SGPR
+__device__ __forceinline__ float sgpr_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
@@ -200,6 +205,18 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     float* Hs = sm + wave * NFP;
+    // the rows' BN3 constants [mu3 inv3 g3 b3] x F2MAX after the waves' Hs rows, read with wave-uniform
+    // 16-byte LDS reads (row-chained scalar loads serialised one L2 round trip per row: the ELU / pool
+    // phase of a trial took ~5 K cycles for ~1 K of work)
+    float* const Ct = sm + nw * NFP;
+    if (tid < F2MAX) {
+        const int j = tid < F2 ? tid : 0;
+        const bool on = tid < F2;
+        Ct[4 * tid + 0] = on ? coef[CF_MU3 * CSTR + j] : 0.f;
+        Ct[4 * tid + 1] = on ? coef[CF_INV3 * CSTR + j] : 0.f;
+        Ct[4 * tid + 2] = on ? prm[g.o_g3 + j] : 0.f;
+        Ct[4 * tid + 3] = on ? prm[g.o_b3 + j] : 0.f;
+    }
 
     float wf[NCLS][NFQ], wacc[NCLS][NFQ];
 #pragma unroll
@@ -217,6 +234,7 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
     const float invB = 1.0f / (float)g.Bn;
     const int bfirst = blockIdx.x * nw + wave, bstop = g.B, bstep = gridDim.x * nw;
 
+    __syncthreads();                          // the constant table
     TRACE(g, 2, TR_PRO);
     TRACE_DECL();
     drain_prologue_loads();
@@ -227,15 +245,21 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
             float r[F2MAX][MQ];
             load_rows<MQ>(r3g, b, F2, T1, lane, r);
             TRACE_PH(g, 2, 0, tph_);
-            bn3_rows<MQ>(coef, F2, r, xh);
+#pragma unroll
+            for (int j = 0; j < F2MAX; ++j) {
+                const floatx4 c = lds_ld4(Ct + 4 * j);
+                const float mu = sgpr_f(c[0]), inv = sgpr_f(c[1]);
+#pragma unroll
+                for (int m = 0; m < MQ; ++m) xh[j][m] = (r[j][m] - mu) * inv;
+            }
             TRACE_PH(g, 2, 1, tph_);
         }
         // ELU -> AvgPool(1,8) -> Hs (flattened index j*T2 + t/8)
 #pragma unroll
         for (int j = 0; j < F2MAX; ++j) {
             if (j >= F2) break;
-            const int oz = opaque0();
-            const float g3 = prm[g.o_g3 + j + oz], b3 = prm[g.o_b3 + j + oz];     // 2 scalars: fine hoisted
+            const floatx4 c = lds_ld4(Ct + 4 * j);
+            const float g3 = sgpr_f(c[2]), b3 = sgpr_f(c[3]);
 #pragma unroll
             for (int m = 0; m < MQ; ++m) {
                 const int t = lane + 64 * m;
@@ -308,8 +332,8 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
 #pragma unroll
             for (int j = 0; j < F2MAX; ++j) {
                 if (j >= F2) break;
-                const int oz = opaque0();
-                const float g3 = prm[g.o_g3 + j + oz], b3 = prm[g.o_b3 + j + oz];
+                const floatx4 c = lds_ld4(Ct + 4 * j);
+                const float g3 = sgpr_f(c[2]), b3 = sgpr_f(c[3]);
 #pragma unroll
                 for (int m = 0; m < MQ; ++m) {
                     const int t = lane + 64 * m;
@@ -666,10 +690,6 @@ __host__ __device__ constexpr int dr_stride(int MQ) { return 64 * MQ + 2; }
 __host__ __device__ constexpr int dr_lds_floats(int MQ) { return 4 * F2MAX * dr_stride(MQ) + F2MAX * (F2MAX + K2); }
 // after the loop: dW3 tiles [NWB][256], the owned row [18 F2MAX], and (T1 = 64) the Hankel tiles
 __host__ __device__ constexpr int dr_tail_floats(bool hankel) { return NWB * 256 + 18 * F2MAX + (hankel ? NWB * RPW * 2 * 256 : 0); }
-
-__device__ __forceinline__ float sgpr_f(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
-}
 
 template <int K1, int CC, int TT, int FF, bool FOLD = false, bool MASK = true>
 __global__ __launch_bounds__(NTB, TT ? WPEB : 2) void k_pass_dr(Geo g, const float* __restrict__ prm,
