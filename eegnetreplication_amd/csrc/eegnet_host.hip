@@ -860,7 +860,7 @@ int eegnet_train_step(const eegnet_dims* dims, float* params, float* bn_buffers,
     if (int r = check_ptrs(grads, "grads", ws, "ws")) return r;
     if (adam_state && !step) return fail(EEGNET_EINVAL, "step is NULL");
     if (flags & ~(EEGNET_NO_CLAMP | EEGNET_KEY_FROM_STEP))
-        return fail(EEGNET_EINVAL, "unknown flags 0x%x (bit 4, the ABI-5 persistent step, was retired in ABI 6)",
+        return fail(EEGNET_EINVAL, "unknown flags 0x%x (bit 4, round 5's opt-in persistent step, is retired)",
                     flags & ~(EEGNET_NO_CLAMP | EEGNET_KEY_FROM_STEP));
     g.noclamp = (flags & EEGNET_NO_CLAMP) ? 1 : 0;
     g.drop = g.p > 0.f ? 1 : 0;

@@ -257,7 +257,7 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
         // ELU -> AvgPool(1,8) -> Hs (flattened index j*T2 + t/8)
 #pragma unroll
         for (int j = 0; j < F2MAX; ++j) {
-            if (j >= F2) break;
+            if (j >= F2) continue;
             const floatx4 c = lds_ld4(Ct + 4 * j);
             const float g3 = sgpr_f(c[2]), b3 = sgpr_f(c[3]);
 #pragma unroll
@@ -331,7 +331,7 @@ __device__ __forceinline__ void pass_c_body(const Geo& g, const float* __restric
             // BN3-backward sums: dz3 = dp3/8 * ELU'(z3)
 #pragma unroll
             for (int j = 0; j < F2MAX; ++j) {
-                if (j >= F2) break;
+                if (j >= F2) continue;
                 const floatx4 c = lds_ld4(Ct + 4 * j);
                 const float g3 = sgpr_f(c[2]), b3 = sgpr_f(c[3]);
 #pragma unroll
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
         const size_t rb = (size_t)b * F2 * T1;
 #pragma unroll
         for (int o = 0; o < F2MAX; ++o) {
-            if (o >= F2) break;
+            if (o >= F2) continue;
             float a[MQ];
             const int oz = o >= 2 ? opaque0_after(sz[o >= 2 ? o - 2 : 0]) : opaque0();
             conv16_same_t<MQ>(dq[o], prm + (g.o_w2 + o * K2 + oz), a, lane);
