@@ -971,16 +971,16 @@ int eegnet_stage_sums(const eegnet_dims* dims, int pass, size_t* offset_bytes, i
 
 }  // extern "C"
 
-// trials per workgroup of the fold-indexed launches: streaming passes A / B / E, passes C / D, the
-// whole-trial block-2 passes (-DEEGNET_B2=1); a -DEEGNET_FOLD_TPW_S / _C / _B2 build overrides them
-// (sweeps).  Chosen by tools/fold_tpw_sweep.py over 90, 36 and 12 resident folds of batch 64 (22 x 257;
-// DESIGN 6.1): 4,8,2 trains 12 folds per GPU (cfg3: 90 folds over 8 GPUs) 1.9x faster than the grid
-// 90 folds on one GPU prefer (13,32,6), at 7 % less on those 90.
+// trials per workgroup of the fold-indexed launches: the streaming-grid passes A / B / D (k_pass_dr) /
+// E, pass C, the whole-trial block-2 passes (-DEEGNET_B2=1); a -DEEGNET_FOLD_TPW_S / _C / _B2 build
+// overrides them (sweeps, tools/r6_tpw.sh).  Chosen over 12, 23, 45 and 90 resident folds of batch 64
+// (22 x 257): 4 trials per streaming workgroup; pass C one trial per wave of its 16 (round 6:
+// 16 instead of 8 left no wave idle, +3 % at 12 folds and +5-6 % at 45 / 90).
 #ifndef EEGNET_FOLD_TPW_S
 #define EEGNET_FOLD_TPW_S 4
 #endif
 #ifndef EEGNET_FOLD_TPW_C
-#define EEGNET_FOLD_TPW_C 8
+#define EEGNET_FOLD_TPW_C 16
 #endif
 #ifndef EEGNET_FOLD_TPW_B2
 #define EEGNET_FOLD_TPW_B2 2
