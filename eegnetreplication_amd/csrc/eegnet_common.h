@@ -74,7 +74,8 @@ struct Geo {
     int QR;              // rows of pass E's lag correlation Q in its partial row: F1 when every wave's
                          // rows share one temporal group (narrow path, D = 2: summed before publishing), else F2
     int grid;            // workgroups of passes C, D and the eval forward
-    int gridS;           // workgroups of the streaming passes A, B, E (two per CU)
+    int gridS;           // workgroups of the streaming passes A, B, D (k_pass_dr), E (two per CU)
+    int gridA, gridE;    // passes A and E: gridS, or their own trials-per-workgroup in fold launches
     // LDS (floats)
     int ldsA, ldsB, ldsC, ldsD, ldsE, ldsI;
     // optional timeline instrumentation (eegnet_trace_enable): [pass][workgroup][TR_SLOTS] stamps

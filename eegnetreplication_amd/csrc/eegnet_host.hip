@@ -151,7 +151,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     g->QR = (g->F2 <= F2MAX && g->D == 2) ? g->F1 : g->F2;
     g->nE = g->QR * g->K1 + g->F2 * g->C + 2 * g->F2;
     g->grid = std::min(g->B, device_cus() * grid_mult_cd());     // passes C, D, infer
-    g->gridS = std::min(g->B, device_cus() * WGPC * grid_mult());     // streaming passes A, B, E
+    g->gridS = std::min(g->B, device_cus() * WGPC * grid_mult());     // streaming passes A, B, D, E
+    g->gridA = g->gridE = g->gridS;
     const int rows1 = g->C * g->RS;                   // x rows (one buffer)
     const int nf4 = rup(g->NF, 4);
     const bool spec = g->C == 22 && (g->T == 256 || g->T == 257) && g->F1 == 8 && g->D == 2 && g->K1 == 32;   // EEG_DISPATCH
@@ -212,6 +213,7 @@ static int make_geo_wide(Geo* g, bool launch) {
     G = std::max(g->NOC, G / g->NOC * g->NOC);
     if (G >= 8 * g->NOC) G = G / (8 * g->NOC) * (8 * g->NOC);
     g->gridS = G;
+    g->gridA = g->gridE = G;
     g->grid = std::min(g->B, cus);                      // block-2 passes and the eval forward
     // partial rows wider than this reduce in k_coltail (column-parallel) instead of in-kernel
     g->splitC = g->nC > SPLIT_COLS; g->splitD = g->nD > SPLIT_COLS; g->splitE = g->nE > SPLIT_COLS;
@@ -251,11 +253,11 @@ static WsLayout make_layout(const Geo& g) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = rupz(o + bytes, 256); return r; };
     L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
-    L.partA = take((size_t)g.gridS * g.nA * 4);
+    L.partA = take((size_t)std::max(g.gridS, g.gridA) * g.nA * 4);
     L.partB = take((size_t)std::max(g.gridS, g.grid) * g.nB * 4);
     L.partC = take((size_t)std::max(g.grid, g.gridB2) * g.nC * 4);
     L.partD = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridS) * g.nD * 4);   // (k_pass_dr: gridS)
-    L.partE = take((size_t)g.gridS * g.nE * 4);
+    L.partE = take((size_t)std::max(g.gridS, g.gridE) * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
     L.sums = take((size_t)nmax * 8 * NGRPMAX);
     L.stats = take((size_t)(g.F1 * g.K1 + g.K1) * 8);   // fin1 -> fin5: G w1 per filter, window sums S1
@@ -488,9 +490,9 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
     if (g.wide) return run_forward_wide<K1>(g, L, ws, params, bn, x, m2, update_running, nbt, s);
     const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
-#define LAUNCH_A(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsA * 4, s, \
+#define LAUNCH_A(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF, true>), dim3(g.gridA, nf), dim3(NTB), g.ldsA * 4, s, \
                                                    g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc); \
-    else hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsA * 4, s, \
+    else hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF>), dim3(g.gridA, nf), dim3(NTB), g.ldsA * 4, s, \
                                                    g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc)
     if (only < 0 || only == 0) { { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
     } LAUNCH_CHECK("k_pass_a"); }
@@ -589,10 +591,10 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     if (only < 0 || only == 3) { { PROF(KID_D); if (EEGNET_D1) EEG_DISPATCH(K1, g, LAUNCH_D); else EEG_DISPATCH(K1, g, LAUNCH_DR);
     } LAUNCH_CHECK("k_pass_d"); }
     }
-#define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
+#define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridE, nf), dim3(NTB), g.ldsE * 4, s, \
                        g, (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v), \
                        (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc); \
-    else hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsE * 4, s, \
+    else hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF>), dim3(g.gridE, nf), dim3(NTB), g.ldsE * 4, s, \
                        g, (const float*)params, coef, x, (const float*)(ws + L.s), (const float*)(ws + L.v), \
                        (const float*)(ws + L.dp2), (float*)(ws + L.partE), fe, fc)
     if (only < 0 || only == 4) { { PROF(KID_E); EEG_DISPATCH(K1, g, LAUNCH_E);
@@ -979,6 +981,12 @@ int eegnet_stage_sums(const eegnet_dims* dims, int pass, size_t* offset_bytes, i
 #ifndef EEGNET_FOLD_TPW_S
 #define EEGNET_FOLD_TPW_S 4
 #endif
+#ifndef EEGNET_FOLD_TPW_A
+#define EEGNET_FOLD_TPW_A EEGNET_FOLD_TPW_S
+#endif
+#ifndef EEGNET_FOLD_TPW_E
+#define EEGNET_FOLD_TPW_E EEGNET_FOLD_TPW_S
+#endif
 #ifndef EEGNET_FOLD_TPW_C
 #define EEGNET_FOLD_TPW_C 16
 #endif
@@ -1011,6 +1019,8 @@ int eegnet_train_step_folds(const eegnet_dims* dims, int nfolds, const eegnet_fo
     // over ranks).  Capped at the non-fold grids the workspace's partial rows are sized for.
     int tpwS, tpwC, tpwB2;
     fold_tpw(&tpwS, &tpwC, &tpwB2);
+    g.gridA = std::max(1, std::min(g.gridS, (g.B + EEGNET_FOLD_TPW_A - 1) / EEGNET_FOLD_TPW_A));
+    g.gridE = std::max(1, std::min(g.gridS, (g.B + EEGNET_FOLD_TPW_E - 1) / EEGNET_FOLD_TPW_E));
     g.gridS = std::max(1, std::min(g.gridS, (g.B + tpwS - 1) / tpwS));
     g.grid = std::max(1, std::min(g.grid, (g.B + tpwC - 1) / tpwC));
     g.gridB2 = std::max(1, std::min(g.gridB2, (g.B + tpwB2 - 1) / tpwB2));
