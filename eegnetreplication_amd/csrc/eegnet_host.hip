@@ -331,12 +331,14 @@ template <int K1, int CC, int TT, int FF>
 static void set_attrs_shape() {
     const int lds = LDS_MAX;
     for (const void* f : {(const void*)k_pass_a<K1, CC, TT, FF>, (const void*)k_pass_b<K1, CC, TT, FF>,
-                          (const void*)k_pass_c<K1, CC, TT, FF>, (const void*)k_pass_d<K1, CC, TT, FF>,
+                          (const void*)k_pass_c<K1, CC, TT, FF>,
                           (const void*)k_pass_e<K1, CC, TT, FF>, (const void*)k_pass_a<K1, CC, TT, FF, true>,
                           (const void*)k_pass_b<K1, CC, TT, FF, true>, (const void*)k_pass_c<K1, CC, TT, FF, true>,
                           (const void*)k_pass_e<K1, CC, TT, FF, true>,
-                          (const void*)k_pass_d<K1, CC, TT, FF, false, false>,
+#if EEGNET_D1
+                          (const void*)k_pass_d<K1, CC, TT, FF>, (const void*)k_pass_d<K1, CC, TT, FF, false, false>,
                           (const void*)k_pass_d<K1, CC, TT, FF, true, false>,
+#endif
                           (const void*)k_pass_dr<K1, CC, TT, FF>, (const void*)k_pass_dr<K1, CC, TT, FF, false, false>,
                           (const void*)k_pass_dr<K1, CC, TT, FF, true, false>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -588,7 +590,12 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
                        (const float*)(ws + L.E2), (const float*)(ws + L.q3), (const float*)(ws + L.r3), \
                        m2, m3, dl, (float*)(ws + L.dp2), \
                        (float*)(ws + L.partD), fd, fc)
-    if (only < 0 || only == 3) { { PROF(KID_D); if (EEGNET_D1) EEG_DISPATCH(K1, g, LAUNCH_D); else EEG_DISPATCH(K1, g, LAUNCH_DR);
+#if EEGNET_D1
+#define LAUNCH_PASS_D LAUNCH_D
+#else
+#define LAUNCH_PASS_D LAUNCH_DR
+#endif
+    if (only < 0 || only == 3) { { PROF(KID_D); EEG_DISPATCH(K1, g, LAUNCH_PASS_D);
     } LAUNCH_CHECK("k_pass_d"); }
     }
 #define LAUNCH_E(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_e<K, CC, TT, FF, true>), dim3(g.gridE, nf), dim3(NTB), g.ldsE * 4, s, \

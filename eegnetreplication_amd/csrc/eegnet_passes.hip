@@ -400,8 +400,10 @@ __global__ __launch_bounds__(TT ? NTH : NTHS) void k_pass_c(Geo g, const float* 
     pass_c_body<K1, CC, TT, FF, FOLD>(g, prm, coef, r3g, mask3, dlin, labels, logits, dlout, part, mode, fa, fc, sm);
 }
 
+#if EEGNET_D1
 // ================================================================================================
 // Pass D: block_2 backward (dW3, dw2), dp2 = d(pooled ELU output), BN2-backward sums.
+// (rounds 1-5; built only by -DEEGNET_D1=1 A/B builds since k_pass_dr replaced it)
 // part row: [dW3 F2*F2][dw2 F2*16][Sdz2 F2][Sdz2x F2]
 // Per-wave LDS rows (stride RSW): P0 d2 (pad LPD) | P1 q, then dq (pad LPQ) | P2 dr (pad LPQ) | Hs [NF].
 // ================================================================================================
@@ -665,6 +667,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
 }
+#endif  // EEGNET_D1
 
 // ================================================================================================
 // Pass D in the streaming passes' row layout (k_pass_dr, the default; k_pass_d above is the
