@@ -244,6 +244,20 @@ struct FoldCall {
 // grid finished its trials in 32 µs and the second half in 53 µs (pass E, B = 4096, r3 stamps), so
 // each CU ran its last ~20 µs at one workgroup's occupancy.  A workgroup drops a priority level per
 // quarter of its range, so the one ahead yields to the one behind.
+// cache policy of the step's plane stores (A/B build options): 1 = nontemporal (the default), 0 = plain
+// stores.  NT_MID: d2/E1/E2 (pass B, read by D) and dp2 (pass D, read by E); NT_SV: s and v (pass A)
+#ifndef EEGNET_NT_MID
+#define EEGNET_NT_MID 1
+#endif
+#ifndef EEGNET_NT_SV
+#define EEGNET_NT_SV 1
+#endif
+template <int NT, typename V>
+__device__ __forceinline__ void st_pol(V v, V* p) {
+    if constexpr (NT != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 #ifndef EEGNET_PRIO
 #define EEGNET_PRIO 1
 #endif

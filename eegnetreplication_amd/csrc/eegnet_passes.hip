@@ -628,7 +628,7 @@ __global__ __launch_bounds__(NTHS) void k_pass_d(Geo g, const float* __restrict_
                 if (t < T1) {
                     const int gi = o * T1 + t;
                     const float dp = a[m] * keep_mul(g, mask2, dk0, (unsigned)(rb + gi));
-                    __builtin_nontemporal_store(dp, dp2g + rb + gi);
+                    st_pol<EEGNET_NT_MID>(dp, dp2g + rb + gi);
                     sz[o] = fmaf(dp * 0.25f, e1v[o][m], sz[o]);
                     sz[F2MAX + o] = fmaf(dp * 0.25f, e2v[o][m], sz[F2MAX + o]);
                 }
@@ -986,7 +986,7 @@ __global__ __launch_bounds__(NTB, TT ? WPEB : 2) void k_pass_dr(Geo g, const flo
                 if (FULL || t < T1) {
                     const int gi = o * T1 + t;
                     const float dp = y[m] * keep_mul(g, mask2, dk0, (unsigned)(rb + gi));
-                    __builtin_nontemporal_store(dp, dp2g + rb + gi);
+                    st_pol<EEGNET_NT_MID>(dp, dp2g + rb + gi);
                     const float dpg = live ? dp * 0.25f : 0.f;
                     sz1[r] = fmaf(dpg, x1[r][m], sz1[r]);
                     sz2[r] = fmaf(dpg, x2[r][m], sz2[r]);

@@ -168,7 +168,7 @@ __device__ __forceinline__ void s_rows_store(const float* Ss, float* __restrict_
     const int TQ4 = s_pitch(T) >> 2;
     for (int i = tid; i < F2 * TQ4; i += NT) {
         const int o = i / TQ4, q = i - o * TQ4;
-        __builtin_nontemporal_store(lds_ld4(Ss + o * RS + LP + 4 * q), reinterpret_cast<floatx4*>(sb + 4 * i));
+        st_pol<EEGNET_NT_SV>(lds_ld4(Ss + o * RS + LP + 4 * q), reinterpret_cast<floatx4*>(sb + 4 * i));
     }
 }
 // rows [0, rows) of one trial's s plane into LDS rows (stride RS, left pad LP), 16-byte LDS-DMA units
@@ -550,8 +550,8 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
 #pragma unroll
                         for (int i = 0; i < 8; ++i)
                             if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
-                        __builtin_nontemporal_store((floatx4){v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
-                        __builtin_nontemporal_store((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
+                        st_pol<EEGNET_NT_SV>((floatx4){v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
+                        st_pol<EEGNET_NT_SV>((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
                     }
                 }
             }
@@ -574,8 +574,8 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
                 for (int m = 0; m < MOA; ++m) {
                     const int oc = fir_oct(lane) + 32 * m;
                     if (oc < NO) {
-                        __builtin_nontemporal_store((floatx4){vs[m][0], vs[m][1], vs[m][2], vs[m][3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
-                        __builtin_nontemporal_store((floatx4){vs[m][4], vs[m][5], vs[m][6], vs[m][7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
+                        st_pol<EEGNET_NT_SV>((floatx4){vs[m][0], vs[m][1], vs[m][2], vs[m][3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
+                        st_pol<EEGNET_NT_SV>((floatx4){vs[m][4], vs[m][5], vs[m][6], vs[m][7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
                     }
                 }
             }
@@ -922,8 +922,8 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
                     const int q = 2 * oc + h;
                     if (q < T1) {
                         const size_t gi = ((size_t)b * F2 + oh) * T1 + q;
-                        __builtin_nontemporal_store(d2v[m][h], d2g + gi); __builtin_nontemporal_store(e1v[m][h], E1g + gi);
-                        __builtin_nontemporal_store(e2v[m][h], E2g + gi);
+                        st_pol<EEGNET_NT_MID>(d2v[m][h], d2g + gi); st_pol<EEGNET_NT_MID>(e1v[m][h], E1g + gi);
+                        st_pol<EEGNET_NT_MID>(e2v[m][h], E2g + gi);
                     }
                 }
             }

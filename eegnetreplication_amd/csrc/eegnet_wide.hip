@@ -248,12 +248,12 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
     auto plane_stores = [&](int bb) {
         const float* rowp = sm + 2 * g.CPC * RS + ((bb - b0) & 1) * 16 * RS + wave * RS;
         float* vrow = vg + ((size_t)bb * F2 + o) * (8 * NO);
-        __builtin_nontemporal_store((floatx4){vd[0], vd[1], vd[2], vd[3]}, reinterpret_cast<floatx4*>(vrow + 8 * lane));
-        __builtin_nontemporal_store((floatx4){vd[4], vd[5], vd[6], vd[7]}, reinterpret_cast<floatx4*>(vrow + 8 * lane + 4));
+        st_pol<EEGNET_NT_SV>((floatx4){vd[0], vd[1], vd[2], vd[3]}, reinterpret_cast<floatx4*>(vrow + 8 * lane));
+        st_pol<EEGNET_NT_SV>((floatx4){vd[4], vd[5], vd[6], vd[7]}, reinterpret_cast<floatx4*>(vrow + 8 * lane + 4));
         float* srow = sg + ((size_t)bb * F2 + o) * s_pitch(T);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            __builtin_nontemporal_store(lds_ld4(rowp + LP + 4 * lane + 256 * q), reinterpret_cast<floatx4*>(srow + 4 * lane + 256 * q));
+            st_pol<EEGNET_NT_SV>(lds_ld4(rowp + LP + 4 * lane + 256 * q), reinterpret_cast<floatx4*>(srow + 4 * lane + 256 * q));
     };
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
@@ -344,14 +344,14 @@ __global__ __launch_bounds__(NTW) void k_wpass_a(Geo gin, const float* __restric
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
                     if (8 * oc + i < T) { svl += v[i]; sv2l = fmaf(v[i], v[i], sv2l); }
-                __builtin_nontemporal_store((floatx4){v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
-                __builtin_nontemporal_store((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
+                st_pol<EEGNET_NT_SV>((floatx4){v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(vrow + 8 * oc));
+                st_pol<EEGNET_NT_SV>((floatx4){v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(vrow + 8 * oc + 4));
             }
             float* srow = sg + ((size_t)b * F2 + o) * s_pitch(T);
             if constexpr (SPEC) { (void)srow; } else
             if ((T & 3) == 0) {
                 for (int t = 4 * lane; t < T; t += 256)
-                    __builtin_nontemporal_store(lds_ld4(row + LP + t), reinterpret_cast<floatx4*>(srow + t));
+                    st_pol<EEGNET_NT_SV>(lds_ld4(row + LP + t), reinterpret_cast<floatx4*>(srow + t));
             } else {
                 for (int t = lane; t < T; t += 64) srow[t] = row[LP + t];
             }
