@@ -83,6 +83,7 @@ struct Geo {
     // F2 > 16 (eegnet_wide.hip): o-chunks of 16 rows, Gram electrode slice per chunk, block-2 rows
     // padded to F2P (32 / 64), block-2 row stride; LDS (floats) of the wide kernels
     int wide, NOC, CPC, F2P, RB, gridB2;
+    int gridW2;          // wide passes B2 and C (whole-job launches): two workgroups per CU at cfg5
     int splitC, splitD, splitE;   // wide passes whose reduction + finalize run in k_coltail (wide rows)
     int ldsWA, ldsWB, ldsWB2, ldsWC, ldsWD, ldsWE, ldsWI;
     // batch the statistics and the CE mean are normalised by: B, or the global batch of a data-parallel
@@ -105,7 +106,7 @@ struct Geo {
     X(o_ws, 544) X(o_g2, 4640) X(o_b2, 4704) X(o_w2, 4768) X(o_W3, 5792) X(o_g3, 9888) X(o_b3, 9952) \
     X(o_Wfc, 10016) X(o_bfc, 14112) X(nparam, 14116) X(nA, 448) X(nB, 128) X(nC, 4229) X(nD, 5248)    \
     X(nE, 6272) X(QR, 64) X(wide, 1) X(NOC, 4) X(CPC, 16) X(F2P, 64) X(RB, 144) X(splitC, 1)         \
-    X(splitD, 1) X(splitE, 1) X(ldsWA, 36656) X(ldsWB, 0) X(ldsWB2, 23872) X(ldsWC, 10528)           \
+    X(splitD, 1) X(splitE, 1) X(ldsWA, 36656) X(ldsWB, 0) X(ldsWB2, 19712) X(ldsWC, 10528)           \
     X(ldsWD, 37952) X(ldsWE, 29504) X(ldsWI, 37760)
 __host__ __device__ __forceinline__ void shape_w5(Geo& g) {
 #define EEG_SET_(f, v) g.f = v;

@@ -231,6 +231,11 @@ static int make_geo_wide(Geo* g, bool launch) {
     const int b2 = 2 * g->F2P * g->RB + g->F2P * K2 + g->F2P * (g->F2P + 1);   // D2, Q, w2, W3 tables
     b2_lds(g, NWB2);
     g->gridB2 = g->grid;
+    // the cfg5 (SPEC) k_wpass_b2 keeps its W3 fragments in registers instead of an LDS table, and it and
+    // k_wpass_c stay within 128 VGPRs: two 8-wave workgroups per CU, two trials each at B = 1024, so one
+    // workgroup's barriers overlap the other's work
+    g->gridW2 = w5 ? std::min(g->B, 2 * cus) : g->grid;
+    if (w5) g->ldsWB2 = std::max(g->ldsWB2 - g->F2P * (g->F2P + 1), tailw(g->nB, 0));
     // s rows, dy / e rows x 2 (alternate trials), dp2 rows, coefficient table
     g->ldsWE = std::max(std::max(3 * 16 * g->RS + rup(16 * g->T1, 4) + 8 * 16 + awl, NWW * 256 + 32 + NWW * 256 * ((15 + g->K1 - 1) / 16 + 1)),
                         tailw(g->nE, fin5_scratch_doubles(g->K1, g->F1, g->o_g2)));
@@ -254,8 +259,8 @@ static WsLayout make_layout(const Geo& g) {
     auto take = [&](size_t bytes) { size_t r = o; o = rupz(o + bytes, 256); return r; };
     L.cnt = take(CNT_BYTES);          // ticket words first: the per-call memset covers [0, CNT_BYTES)
     L.partA = take((size_t)std::max(g.gridS, g.gridA) * g.nA * 4);
-    L.partB = take((size_t)std::max(g.gridS, g.grid) * g.nB * 4);
-    L.partC = take((size_t)std::max(g.grid, g.gridB2) * g.nC * 4);
+    L.partB = take((size_t)std::max(std::max(g.gridS, g.grid), g.gridW2) * g.nB * 4);
+    L.partC = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridW2) * g.nC * 4);
     L.partD = take((size_t)std::max(std::max(g.grid, g.gridB2), g.gridS) * g.nD * 4);   // (k_pass_dr: gridS)
     L.partE = take((size_t)std::max(g.gridS, g.gridE) * g.nE * 4);
     const int nmax = std::max(std::max(std::max(g.nA, g.nB), std::max(g.nC, g.nD)), g.nE);
@@ -358,7 +363,7 @@ static void ensure_attrs() {
     set_attrs_wide<64>();
     for (const void* f : {(const void*)k_wpass_a<32, true>, (const void*)k_wpass_b<32, true>, (const void*)k_wpass_e<32, true>,
                           (const void*)k_winfer<32, true>, (const void*)k_wpass_b2<NTB2, true>,
-                          (const void*)k_wpass_c<NTB2, false, true>, (const void*)k_wpass_d<NTB2, false, true>,
+                          (const void*)k_wpass_c<NTB2, false, true>, (const void*)k_wpass_d<NTD5, false, true>,
                           (const void*)k_coltail<3, true>, (const void*)k_coltail<4, true>, (const void*)k_coltail<5, true>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_wpass_b2<NTB2>, (const void*)k_wpass_c<NTB2>, (const void*)k_wpass_d<NTB2>,
@@ -433,7 +438,7 @@ static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const flo
     { PROF(KID_WB); WLAUNCH(sp, (k_wpass_b<K1>), (k_wpass_b<K1, K1 == 32>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g,
                             params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2),
                             (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
-    { PROF(KID_WB2); WLAUNCH(sp, k_wpass_b2<NTB2>, (k_wpass_b2<NTB2, true>), dim3(g.grid), dim3(NTB2), g.ldsWB2 * 4, s,
+    { PROF(KID_WB2); WLAUNCH(sp, k_wpass_b2<NTB2>, (k_wpass_b2<NTB2, true>), dim3(g.gridW2), dim3(NTB2), g.ldsWB2 * 4, s,
                              g, params, (const float*)(ws + L.d2), (float*)(ws + L.q3), (float*)(ws + L.r3),
                              (float*)(ws + L.partB), fb); } LAUNCH_CHECK("k_wpass_b2");
     return 0;
@@ -463,11 +468,11 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
         else if (fin == 4) WLAUNCH(sp, k_coltail<4>, (k_coltail<4, true>), dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
         else WLAUNCH(sp, k_coltail<5>, (k_coltail<5, true>), dim3(nb), dim3(NTCT), lds, s, g, (const float*)params, part, nrows, ncols, fa);
     };
-    { PROF(KID_WC); WLAUNCH(sp, k_wpass_c<NTB2>, (k_wpass_c<NTB2, false, true>), dim3(g.grid), dim3(NTB2), g.ldsWC * 4, s,
+    { PROF(KID_WC); WLAUNCH(sp, k_wpass_c<NTB2>, (k_wpass_c<NTB2, false, true>), dim3(g.gridW2), dim3(NTB2), g.ldsWC * 4, s,
                             g, params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits, (float*)(ws + L.dl),
                             (float*)(ws + L.partC), c_mode, fc, FoldCall{}); } LAUNCH_CHECK("k_wpass_c(bwd)");
-    if (g.splitC) { coltail(3, (const float*)(ws + L.partC), g.grid, g.nC, fc, 0); LAUNCH_CHECK("k_coltail(C)"); }
-    { PROF(KID_WD); WLAUNCH(sp, k_wpass_d<NTB2>, (k_wpass_d<NTB2, false, true>), dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s,
+    if (g.splitC) { coltail(3, (const float*)(ws + L.partC), g.gridW2, g.nC, fc, 0); LAUNCH_CHECK("k_coltail(C)"); }
+    { PROF(KID_WD); WLAUNCH(sp, k_wpass_d<NTB2>, (k_wpass_d<NTD5, false, true>), dim3(g.grid), dim3(sp ? NTD5 : NTB2), g.ldsWD * 4, s,
                             g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
                             (const float*)(ws + L.q3), (const float*)(ws + L.r3), m2, m3, dl,
                             (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
@@ -744,7 +749,7 @@ int eegnet_forward_train(const eegnet_dims* dims, const float* params, float* bn
     memset(&none, 0, sizeof(none));
     if (g.wide) {
         const bool sp = g.K1 == 32 && same_shape_w5(g);
-        { PROF(KID_WC); WLAUNCH(sp, k_wpass_c<NTB2>, (k_wpass_c<NTB2, false, true>), dim3(g.grid), dim3(NTB2),
+        { PROF(KID_WC); WLAUNCH(sp, k_wpass_c<NTB2>, (k_wpass_c<NTB2, false, true>), dim3(g.gridW2), dim3(NTB2),
                                 g.ldsWC * 4, s, g, params, (const float*)(w + L.coef), (const float*)(w + L.r3), mask3,
                                 (const float*)nullptr, (const int64_t*)nullptr, logits, (float*)nullptr,
                                 (float*)nullptr, (int)PC_LOGITS, none, FoldCall{}); }

@@ -1000,6 +1000,11 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 #ifndef EEGNET_LDSX_E
 #define EEGNET_LDSX_E 0
 #endif
+// EEGNET_E_XTOP = 1 (A/B builds): the pipelined shape (PIPEE) issues the trial's x DMA at the top of
+// the trial, right after the previous closing barrier freed the x buffer, instead of after dy2
+#ifndef EEGNET_E_XTOP
+#define EEGNET_E_XTOP 0
+#endif
 template <int K1, int CC, int TT, int FF, bool FOLD>
 __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   // Adam (finalize) writes it
                                             const float* coef,    // the finalize writes it: no __restrict__
@@ -1177,6 +1182,12 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
         pace_prio(b - b0, b1 - b0);
+        if constexpr (PIPEE && EEGNET_E_XTOP) {
+            // vmcnt is 0 here (the previous closing barrier); the explicit wait tells the compiler so,
+            // or its wait for vpf at the first use would count this asm DMA as older work
+            __builtin_amdgcn_s_waitcnt(0);
+            if (EEGNET_LDSX_E != 7) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
+        }
         float vc[MO][8];
         if constexpr (VPF) {
 #pragma unroll
@@ -1234,7 +1245,7 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
         }
         // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
         // GEMM); they land during the lag correlation / FIR^T, by the next barrier
-        if constexpr (XDMA)
+        if constexpr (XDMA && !(PIPEE && EEGNET_E_XTOP))
             if (EEGNET_LDSX_E != 7) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 2, tph_);
         {

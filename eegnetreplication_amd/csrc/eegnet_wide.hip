@@ -30,6 +30,12 @@ constexpr int NTW = 1024;              // threads of the wide streaming passes a
 constexpr int NWW = NTW / 64;          // = 16 rows of an o-chunk, one per wave
 constexpr int NTB2 = 512;              // threads of the wide block-2 passes (8 waves)
 constexpr int NWB2 = NTB2 / 64;
+// threads of the cfg5 (SPEC) wide pass D: 512 (one 8-wave workgroup per CU, 255 VGPRs) or, A/B builds
+// -DEEGNET_WD_NT=1024, 16 waves per CU at <= 128 VGPRs
+#ifndef EEGNET_WD_NT
+#define EEGNET_WD_NT 512
+#endif
+constexpr int NTD5 = EEGNET_WD_NT;
 constexpr int LQW = 8;                 // left pad of block-2 rows (dw16 reads t-7, its transpose t+7)
 constexpr int KSW = 16;                // spatial GEMM k-steps: C <= 64
 constexpr int MAXNOC = 4;              // o-chunks: F2 <= 64
@@ -652,14 +658,24 @@ __global__ __launch_bounds__(NT) void k_wpass_b2(Geo gin, const float* __restric
     float* Q = D2 + F2P * RB;
     float* W2s = Q + F2P * RB;
     float* W3s = W2s + F2P * K2;
-    float* ws_ = W3s + F2P * (F2P + 1);
+    // cfg5: each wave's W3 fragments (row tile mp.jt, all 16 k-steps) live in 16 registers instead of
+    // an LDS table, so two workgroups fit per CU (make_geo_wide: ldsWB2 without the table, gridW2)
+    constexpr bool W3R = SPEC && NT == 512;
+    float* ws_ = W3R ? W3s : W3s + F2P * (F2P + 1);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     for (int i = tid; i < 2 * F2P * RB; i += NT) sm[i] = 0.f;
     load_w2s(g, prm, W2s, F2P, tid, NT);
-    stage_w3(g, prm, W3s, F2P, tid, NT);
     const B2Map mp = b2_map(NJT, wave, NT / 64);
+    float w3r[W3R ? MAXKS3 : 1];
+    if constexpr (W3R) {
+        static_assert(!W3R || MAXKS3 * 4 == 64, "cfg5: F2 = F2P = 64");
+#pragma unroll
+        for (int k = 0; k < MAXKS3; ++k) w3r[k] = prm[g.o_W3 + (16 * mp.jt + li) * F2 + 4 * k + lk];
+    } else {
+        stage_w3(g, prm, W3s, F2P, tid, NT);
+    }
     float sr[4] = {0.f, 0.f, 0.f, 0.f}, sr2[4] = {0.f, 0.f, 0.f, 0.f};
     constexpr bool PF = SPEC && NT == 512;             // cfg5: d2 rows a trial ahead in registers
     floatx4 pd2[PF ? B2PF : 1];
@@ -679,7 +695,21 @@ __global__ __launch_bounds__(NT) void k_wpass_b2(Geo gin, const float* __restric
         __syncthreads();
         const size_t rb = (size_t)b * F2 * T1;
         floatx4 acc[NTTW];
-        b2_pw<NTTW>(Q, W3s, F2P, NT1, RB, mp, acc, lane);
+        if constexpr (W3R) {
+#pragma unroll
+            for (int i = 0; i < NTTW; ++i) {
+                const int n = mp.n0 + mp.dn * i;
+                floatx4 a = {0.f, 0.f, 0.f, 0.f};
+                if (n < NT1) {
+                    const float* qc = Q + lk * RB + LQW + 16 * n + li;
+#pragma unroll
+                    for (int k = 0; k < MAXKS3; ++k) a = __builtin_amdgcn_mfma_f32_16x16x4f32(w3r[k], qc[4 * k * RB], a, 0, 0, 0);
+                }
+                acc[i] = a;
+            }
+        } else {
+            b2_pw<NTTW>(Q, W3s, F2P, NT1, RB, mp, acc, lane);
+        }
 #pragma unroll
         for (int i = 0; i < NTTW; ++i) {
             const int n = mp.n0 + mp.dn * i, t = 16 * n + li;
@@ -739,7 +769,7 @@ __device__ __forceinline__ void b2_bn3(const float* coef, const B2Map& mp, float
 // LDS: H [NF] (features, then their gradients) | class partials [(NT / 64)][4] | sums | XH [F2P][RB]
 // ================================================================================================
 template <int NT, bool FOLD = false, bool SPEC = false>
-__global__ __launch_bounds__(NT) void k_wpass_c(Geo gin, const float* __restrict__ prm, const float* coef,
+__global__ __launch_bounds__(NT, (SPEC && NT == 512) ? 4 : 1) void k_wpass_c(Geo gin, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ r3g, const uint8_t* __restrict__ mask3,
                                                   const float* __restrict__ dlin, const int64_t* __restrict__ labels,
                                                   float* __restrict__ logits, float* __restrict__ dlout,
@@ -955,7 +985,7 @@ __global__ __launch_bounds__(NT) void k_wpass_c(Geo gin, const float* __restrict
 // LDS: D2 [F2P][RB] | Q [F2P][RB] (q, then dq) | DR [F2P][RB] | W2s | Hd [NF] | item sums
 // ================================================================================================
 template <int NT, bool FOLD = false, bool SPEC = false>
-__global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restrict__ prm, const float* coef,
+__global__ __launch_bounds__(NT, NT == 1024 ? 4 : 2) void k_wpass_d(Geo gin, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ d2g, const float* __restrict__ E1g,
                                                   const float* __restrict__ E2g, const float* __restrict__ q3g,
                                                   const float* __restrict__ r3g, const uint8_t* __restrict__ mask2,
@@ -1029,8 +1059,8 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
     // per thread and plane, loaded into registers a whole trial ahead and stored to LDS at the top of
     // the trial; the dd2 phase loads its items' E1 / E2 two items at a time (each of the four items
     // waited one global round trip for them; all four at once, or from the top of the trial, spill)
-    constexpr bool PFD = SPEC && NT == 512;
-    constexpr int NPD = 4;                             // float4 per thread and plane at cfg5
+    constexpr bool PFD = SPEC && (NT == 512 || NT == 1024);
+    constexpr int NPD = 2048 / NT;                     // float4 per thread and plane at cfg5
     floatx4 pd[PFD ? 3 : 1][PFD ? NPD : 1], pe1[PFD ? NPD : 1], pe2[PFD ? NPD : 1];
     auto planes_load = [&](int bb) {
         if constexpr (PFD) {               // (the only caller; keeps the 1 x 1 arrays of !PFD unindexed)
@@ -1174,6 +1204,7 @@ __global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restr
             IS[nit + it] += s2;
         };
         if constexpr (PFD) {
+            static_assert(NPD % 2 == 0, "two dd2 items per round trip");
 #pragma unroll
             for (int h = 0; h < NPD; h += 2) {         // two items' E1 / E2 per round trip
 #pragma unroll

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
        "-fno-slp-vectorize", "-Wno-unused-result", "-Wno-unused-value", "-I", os.path.join(ROOT, "include"),
        "-o", "/tmp/_ru.so", os.path.join(ROOT, "eegnetreplication_amd", "csrc", "eegnet_kernels.hip"),
-       "-Rpass-analysis=kernel-resource-usage"] + (["-DEEGNET_TRACE"] if os.environ.get("TRACE") else [])
+       "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("EXTRA", "").split() + (["-DEEGNET_TRACE"] if os.environ.get("TRACE") else [])
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 filt = sys.argv[1] if len(sys.argv) > 1 else "ILi32ELi22ELi256E"
 rows, cur = {}, None
