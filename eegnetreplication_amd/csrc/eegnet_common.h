@@ -323,6 +323,14 @@ __host__ __device__ constexpr int rup4(int a) { return (a + 3) & ~3; }
 __host__ __device__ constexpr int imax(int a, int b) { return a > b ? a : b; }
 // row pitch of the s plane [B][F2][s_pitch(T)] (floats): T rounded up to 4, so rows are 16-byte units
 __host__ __device__ constexpr int s_pitch(int T) { return (T + 3) & ~3; }
+// EEGNET_NOV = 1: the 22 x 256 EEGNet-8,2 shape keeps no v plane -- pass A stores only s, passes B
+// and E recompute v = FIR(s) from s rows in LDS with pass A's own fir8 (bit-identical v)
+#ifndef EEGNET_NOV
+#define EEGNET_NOV 0
+#endif
+__host__ __device__ constexpr bool nov_shape(int K1, int CC, int TT, int FF) {
+    return EEGNET_NOV && K1 == 32 && CC == 22 && TT == 256 && FF == 16;
+}
 
 __host__ __device__ constexpr int row_stride(int K1, int T) {
     // rows of x / s / dy / e: [LP zeros | T samples | >= R zeros]; long enough for the last 4-output

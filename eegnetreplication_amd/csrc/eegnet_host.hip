@@ -173,6 +173,8 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
     auto tail = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + std::max(tail_scratch_doubles(ncols), fin)); };
     g->ldsA = std::max(g->ldsA, tail(g->nA, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C)));
+    // nov_shape: pass B stages the s rows [F2][RS] it recomputes v from
+    if (nov_shape(g->K1, g->C, g->T, (g->F1 == 8 && g->D == 2) ? 16 : 0)) g->ldsB += g->F2 * g->RS;
     g->ldsB = std::max(g->ldsB, tail(g->nB, 0));
     g->ldsC = std::max(g->ldsC, tail(g->nC, 0));
     g->ldsD = std::max(g->ldsD, tail(g->nD, 0));
@@ -504,11 +506,11 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
     if (only < 0 || only == 0) { { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
     } LAUNCH_CHECK("k_pass_a"); }
 #define LAUNCH_B(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
-                       g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
+                       g, params, (const float*)(ws + L.coef), (const float*)(ws + (nov_shape(K, CC, TT, FF) ? L.s : L.v)), m2, (float*)(ws + L.d2), \
                        (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
                        (float*)(ws + L.partB), fb, fc); \
     else hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
-                       g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
+                       g, params, (const float*)(ws + L.coef), (const float*)(ws + (nov_shape(K, CC, TT, FF) ? L.s : L.v)), m2, (float*)(ws + L.d2), \
                        (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
                        (float*)(ws + L.partB), fb, fc)
     if (only < 0 || only == 1) { { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);

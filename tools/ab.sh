@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for i in 1 2; do
+for i in $(seq 1 ${ITERS:-2}); do
   for lib in ${LIBS:-libeegnet_hip_base.so libeegnet_hip.so}; do
     EEGNET_LIB=$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-infer ${BENCH_ARGS} > gpurun_out/ab_${lib}_$i.log 2>&1 || { echo BENCH_FAILED $lib; tail -20 gpurun_out/ab_${lib}_$i.log; exit 1; }
     LIB=$lib python - <<'PY'
