@@ -305,14 +305,20 @@ static const char* kKernelNames[KID_COUNT] = {"k_pass_a", "k_pass_b", "k_pass_c"
                                               "k_adam", "k_infer", "memset_tickets", "k_infer_bf16",
                                               "k_wpass_a", "k_wpass_b", "k_wpass_b2", "k_wpass_c", "k_wpass_d",
                                               "k_wpass_e", "k_winfer", "k_coltail", "k_xstats"};
+#ifndef EEGNET_PROF_EVENT_FLAGS
+#define EEGNET_PROF_EVENT_FLAGS hipEventDisableSystemFence
+#endif
 struct ProfRec { int kid; hipEvent_t a, b; };
 struct ProfState { unsigned mask = 0; std::vector<ProfRec> recs; std::vector<hipEvent_t> pool; };
 static thread_local ProfState g_prof;
 
 static hipEvent_t prof_event() {
     if (!g_prof.pool.empty()) { hipEvent_t e = g_prof.pool.back(); g_prof.pool.pop_back(); return e; }
+    // timing-only markers: without the system-scope release fence a default event record carries
+    // (an L2 writeback + invalidate around the bracketed kernel, ~4 % of a cfg2 step with k_pass_e
+    // bracketed every step: profiles/r6zb_event_fence.txt); the times are read after a full device sync
     hipEvent_t e;
-    hipEventCreate(&e);
+    hipEventCreateWithFlags(&e, EEGNET_PROF_EVENT_FLAGS);
     return e;
 }
 struct ProfScope {
