@@ -144,6 +144,7 @@ __device__ __forceinline__ void trial_range(const Geo& g, int& b0, int& b1) {
     b1 = (int)((w + 1) * g.B / G);
 }
 
+
 // fine stamps of the reduction / finalize critical path (row TR_FINE + pass, slot k), thread 0 only
 constexpr int TR_FINE = 6;
 #define TRACE_FS(g_, pass_, k_)                                                                  \
@@ -222,7 +223,38 @@ struct FinArgs {
     float* adam_v;
     int32_t* step;
     float lr, b1, b2, eps;
+    // the next pass's first-trial rows of this workgroup's trial range (whole-batch launches of the
+    // streaming grid: the next pass runs the same grid, so its workgroup blockIdx.x lands on this XCD):
+    // read into L2 by the workgroups that lose the reduction ticket, after it (l2_warm_next); null = none
+    const float* warm[3];
+    int warm_n[3];                // floats per trial of warm[k]
 };
+
+// EEGNET_L2WARM = 1 (A/B builds; measured neutral -- pass E's prologue did not shorten and pass D's end
+// waited for the loads: profiles/r6ze_ab_l2warm.txt)
+#ifndef EEGNET_L2WARM
+#define EEGNET_L2WARM 0
+#endif
+// read the next pass's first-trial rows of this workgroup's trial range (FinArgs::warm) into this XCD's
+// L2: one 16-byte load per lane per 1 KiB, kept alive by an empty asm use.  Called by the workgroups
+// that lost the reduction ticket, so the winner's reduction and finalize stay the critical path; the
+// next pass's prologue then finds them in L2 instead of HBM.
+__device__ __forceinline__ void l2_warm_next(const Geo& g, const FinArgs& fa) {
+    if (!EEGNET_L2WARM) return;
+    int b0, b1;
+    trial_range(g, b0, b1);
+    if (b0 >= b1) return;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (!fa.warm[k]) continue;
+        const int n = fa.warm_n[k];
+        const float* p = fa.warm[k] + (size_t)b0 * n;
+        for (int i = 4 * (int)threadIdx.x; i < n; i += 4 * (int)blockDim.x)
+            acc += reinterpret_cast<const floatx4*>(p + i)[0][0];
+    }
+    asm volatile("" :: "v"(acc));
+}
 
 // ticket blocks of the five passes in a workspace
 enum { TK_A = 0, TK_B, TK_C, TK_D, TK_E, TK_COUNT };
@@ -315,6 +347,8 @@ __device__ __forceinline__ FinArgs fold_fin(const FoldCall& fc, const eegnet_fol
     a.adam_v = adam ? f.adam_state + nparam : nullptr;
     a.step = adam ? f.step : nullptr;
     a.lr = fc.lr; a.b1 = fc.b1; a.b2 = fc.b2; a.eps = fc.eps;
+    a.warm[0] = a.warm[1] = a.warm[2] = nullptr;
+    a.warm_n[0] = a.warm_n[1] = a.warm_n[2] = 0;
     return a;
 }
 

@@ -503,7 +503,10 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
                        const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s,
                        const FoldCall& fc = FoldCall{}, int nf = 1, int only = -1) {
     if (g.wide) return run_forward_wide<K1>(g, L, ws, params, bn, x, m2, update_running, nbt, s);
-    const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
+    FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
+    // pass B reads the v plane (the s plane at nov_shape) a trial range per workgroup on the same grid
+    if (nov_shape(g.K1, g.C, g.T, (g.F1 == 8 && g.D == 2) ? 16 : 0)) { fa.warm[0] = (const float*)(ws + L.s); fa.warm_n[0] = g.F2 * s_pitch(g.T); }
+    else { fa.warm[0] = (const float*)(ws + L.v); fa.warm_n[0] = g.F2 * ((g.T + 7) / 8 * 8); }
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
 #define LAUNCH_A(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF, true>), dim3(g.gridA, nf), dim3(NTB), g.ldsA * 4, s, \
                                                    g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc); \
@@ -537,7 +540,11 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     const float* coef = (const float*)(ws + L.coef);
     const float* dl = dlogits ? dlogits : (const float*)(ws + L.dl);
     const FinArgs fcC = fin_args(L, ws, TK_C, nullptr, grads, loss, 0, (c_mode & PC_CE) ? 1 : 0);
-    const FinArgs fd = fin_args(L, ws, TK_D, nullptr, grads, nullptr, 0, 0);
+    FinArgs fd = fin_args(L, ws, TK_D, nullptr, grads, nullptr, 0, 0);
+    // pass E's prologue rows (s, v, dp2 of its first trial) on k_pass_dr's grid, which is pass E's
+    fd.warm[0] = (const float*)(ws + L.s); fd.warm_n[0] = g.F2 * s_pitch(g.T);
+    fd.warm[1] = (const float*)(ws + L.v); fd.warm_n[1] = g.F2 * ((g.T + 7) / 8 * 8);
+    fd.warm[2] = (const float*)(ws + L.dp2); fd.warm_n[2] = g.F2 * g.T1;
     FinArgs fe = fin_args(L, ws, TK_E, nullptr, grads, nullptr, 0, 0);
     if (adam) {
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;

@@ -657,6 +657,8 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
         if (grid_reduce(g, part, g.nA, fa, dsm)) {
             fin1_body<K1, true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa, f1);
             TRACE(g, 0, TR_FIN);
+        } else if (!FOLD) {
+            l2_warm_next(g, fa);                       // pass B's first v rows of this trial range
         }
     }
 }
