@@ -101,6 +101,13 @@ def main():
                 print("    tail stamps (µs after the loop, mean over workgroups): "
                       "waves joined %.2f | sdz reduced %.2f | rows in LDS %.2f | row published %.2f"
                       % tuple(np.mean(ps[:, k] - loop) / 100 for k in range(4)))
+        if os.environ.get("SLOWEST"):
+            # the workgroups whose loops end last: index, XCD (index mod 8), entry, prologue and loop (µs)
+            le = loop - t0
+            idx = np.argsort(-le)[:8]
+            print("    last loop ends:", " ".join(f"wg{i}(x{i % 8}) e{(ent[i]-t0)/100:.1f} p{(pro[i]-ent[i])/100:.1f} l{(loop[i]-pro[i])/100:.1f}" for i in idx))
+            bx = [np.mean((loop - pro)[np.arange(len(loop)) % 8 == x]) / 100 for x in range(8)]
+            print("    loop avg by XCD:", " ".join(f"{v:.1f}" for v in bx), "| wg0 loop", f"{(loop[0]-pro[0])/100:.1f}", "prologue", f"{(pro[0]-ent[0])/100:.1f}")
         ph = st[:, 8:16].mean(axis=0) / ntr
         if ph.any():
             print("    in-loop phases (shader cycles per trial, wave 0):", " ".join(f"{v:.0f}" for v in ph))
