@@ -791,7 +791,7 @@ def main():
                 folds["cpu_baseline"] = real_cpu
         cfg5 = None
         if not args.no_cfg5:
-            cfg5 = bench_train_cfg5(dev, args.cfg5_batch, steps=10, warmup=3)
+            cfg5 = bench_train_cfg5(dev, args.cfg5_batch, steps=30, warmup=3)
         eval2 = None
         if not args.no_infer:
             eval2 = bench_infer_fp32(dev, B, C, T, steps=20, warmup=3)
