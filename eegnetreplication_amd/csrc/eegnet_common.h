@@ -278,7 +278,9 @@ struct FoldCall {
 // each CU ran its last ~20 µs at one workgroup's occupancy.  A workgroup drops a priority level per
 // quarter of its range, so the one ahead yields to the one behind.
 // cache policy of the step's plane stores (A/B build options): 1 = nontemporal (the default), 0 = plain
-// stores.  NT_MID: d2/E1/E2 (pass B, read by D) and dp2 (pass D, read by E); NT_SV: s and v (pass A)
+// stores, 2 = nontemporal at system scope (sc0 sc1 nt: written through, so no dirty plane lines are
+// left in L2 for the kernel's end-of-launch release).  NT_MID: d2/E1/E2 (pass B, read by D) and dp2
+// (pass D, read by E); NT_SV: s and v (pass A)
 #ifndef EEGNET_NT_MID
 #define EEGNET_NT_MID 1
 #endif
@@ -287,8 +289,16 @@ struct FoldCall {
 #endif
 template <int NT, typename V>
 __device__ __forceinline__ void st_pol(V v, V* p) {
-    if constexpr (NT != 0) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    if constexpr (NT == 2) {
+        if constexpr (sizeof(V) == 16)
+            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" :: "v"(p), "v"(v) : "memory");
+        else
+            asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" :: "v"(p), "v"(v) : "memory");
+    } else if constexpr (NT != 0) {
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
 }
 
 #ifndef EEGNET_PRIO
