@@ -42,6 +42,12 @@ CFG4_GLOBAL_BATCH = 65536        # BASELINE configs[3]
 MIN_UNTIMED = 60
 
 
+def settle_steps(warmup, survey, prof):
+    """Untimed settle steps after the W warm-up and the survey (5 event-bracketed steps + the one that
+    fills the event pool), so that at least MIN_UNTIMED untimed steps precede the timed region."""
+    return max(0, MIN_UNTIMED - warmup - (survey + 1 if prof else 0))
+
+
 def kernel_alg_bytes(C=22, T=256, wide=False):
     """SURVEY 8(d)'s algorithmic HBM bytes per trial, attributed to the kernels that need them: x
     is read once for the forward (pass A) and once for the weight gradients (pass E); the labels
@@ -752,7 +758,7 @@ def main():
     alg = kernel_algorithmic(C, T)
     alg_k, ab_k = alg, kernel_alg_bytes(C, T)
     # at least MIN_UNTIMED untimed steps in all (warm-up + survey + settle) before the K timed ones
-    settle = max(0, MIN_UNTIMED - args.warmup - (args.survey + 1 if prof else 0))
+    settle = settle_steps(args.warmup, args.survey, prof)
     dt, table, dom, dk = timed_steps(trainer, xs, ys, args.steps, alg_k, B, barrier, prof, args.survey, settle)
     loss = float(trainer.loss.item())
 
