@@ -121,7 +121,7 @@ class DataParallelTrainer:
         """Rank 0's parameters, BN running statistics and num_batches_tracked to every rank, as ONE
         float64 broadcast (fp32 and the int64 counters below 2^53 round-trip exactly)."""
         m = self.model
-        flat, bn, nbt = m.flat_parameters(), m.flat_bn_buffers(), m.flat_num_batches_tracked()
+        flat, bn, nbt = m.flat_views()
         buf = torch.cat([flat.detach().double(), bn.double(), nbt.double()])
         dist.broadcast(buf, self._src(0), group=self.group)
         n, nb = flat.numel(), bn.numel()
@@ -140,9 +140,10 @@ class DataParallelTrainer:
     # -- stages ------------------------------------------------------------------------------
     def local_grads(self, x, y, seed, offset):
         m = self.model
-        ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
+        flat, bn, nbt = m.flat_views()
+        ops.train_step(m.shape, flat, bn, x, y, seed, offset,
                        self.adam.grads, None, None, self.workspace(x.shape[0]), self.loss,
-                       clamp=False, nbt=m.flat_num_batches_tracked())
+                       clamp=False, nbt=nbt)
         return self.adam.grads
 
     def reduce(self, grads):

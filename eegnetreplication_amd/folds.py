@@ -101,12 +101,13 @@ class FoldBatch:
         m = self.models[k]
         a = self.adam[k]
         Xp, yp = X.index_select(0, perm), y.index_select(0, perm)
+        flat, bn, nbt = m.flat_views()
         for j, i in enumerate(range(0, perm.shape[0], batch_size)):
             xb, yb = Xp[i:i + batch_size], yp[i:i + batch_size]
-            ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), xb, yb, self.seeds[k],
+            ops.train_step(m.shape, flat, bn, xb, yb, self.seeds[k],
                            0, a.grads, a.state, a.step, self._workspace(k, xb.shape[0]),
                            losses[j:j + 1], lr=self.lr, betas=self.betas, eps=self.eps,
-                           nbt=m.flat_num_batches_tracked(), key_from_step=True)
+                           nbt=nbt, key_from_step=True)
 
     def _fold_key(self, k, X, y, batch_size):
         """What fold k's captured epoch baked in: its model / Adam buffers (re-created by ``.to()``,

@@ -110,6 +110,19 @@ class EEGNet(nn.Module):
         self._plist = params
         self._blist = [t for bn in self._bns() for t in (bn.running_mean, bn.running_var)]
         self._nlist = [bn.num_batches_tracked for bn in self._bns()]
+        # every view's expected address, computed once: _flat_ok compares data_ptr() only
+        base, o, ptrs = flat.data_ptr(), 0, []
+        for q in params:
+            ptrs.append(base + 4 * o)
+            o += q.numel()
+        b = bflat.data_ptr()
+        bptrs, o = [], 0
+        for t in self._blist:
+            bptrs.append(b + 4 * o)
+            o += t.numel()
+        self._pexpect = list(zip(params, ptrs))
+        self._bexpect = list(zip(self._blist, bptrs))
+        self._nexpect = [(t, nflat.data_ptr() + 8 * i) for i, t in enumerate(self._nlist) if t is not None]
         self._shape_cache = None
 
     def _apply(self, fn, recurse=True):
@@ -129,23 +142,23 @@ class EEGNet(nn.Module):
             if bn.running_mean is not self._blist[2 * i] or bn.running_var is not self._blist[2 * i + 1] \
                     or bn.num_batches_tracked is not self._nlist[i]:
                 return False
-        base = self._flat.data_ptr()
-        o = 0
-        for p in self._plist:
-            if p.data_ptr() != base + 4 * o or not p.is_contiguous():
+        for p, ptr in self._pexpect:
+            if p.data_ptr() != ptr or not p.is_contiguous():
                 return False
-            o += p.numel()
-        b = self._bn_flat.data_ptr()
-        o = 0
-        for t in self._blist:
-            if t.data_ptr() != b + 4 * o:
+        for t, ptr in self._bexpect:
+            if t.data_ptr() != ptr:
                 return False
-            o += t.numel()
-        n = self._nbt_flat.data_ptr()
-        for i, t in enumerate(self._nlist):
-            if t is not None and t.data_ptr() != n + 8 * i:
+        for t, ptr in self._nexpect:
+            if t.data_ptr() != ptr:
                 return False
         return True
+
+    def flat_views(self):
+        """(flat parameters, flat BN buffers, num_batches_tracked buffer) after ONE layout check (a
+        fused step needs all three; the check is the larger part of its host time)."""
+        if not self._flat_ok():
+            self._flatten()
+        return self._flat, self._bn_flat, self._nbt_flat
 
     def flat_parameters(self) -> torch.Tensor:
         if not self._flat_ok():
@@ -351,10 +364,11 @@ class FusedTrainer:
     def step(self, x, y, logits=None):
         m = self.model
         seed, offset = m.next_dropout_key()
-        ops.train_step(m.shape, m.flat_parameters(), m.flat_bn_buffers(), x, y, seed, offset,
+        flat, bn_flat, nbt = m.flat_views()
+        ops.train_step(m.shape, flat, bn_flat, x, y, seed, offset,
                        self.adam.grads, self.adam.state, self.adam.step, self.workspace(x.shape[0]),
                        self.loss, logits=logits, lr=self.lr, betas=self.betas, eps=self.eps,
-                       nbt=m.flat_num_batches_tracked())
+                       nbt=nbt)
         return self.loss
 
 
