@@ -443,7 +443,9 @@ static int run_forward_wide(const Geo& g, const WsLayout& L, char* ws, const flo
     { PROF(KID_WA); WLAUNCH(sp, (k_wpass_a<K1>), (k_wpass_a<K1, K1 == 32>), dim3(g.gridS), dim3(NTW), g.ldsWA * 4, s, g,
                             params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa); }
     LAUNCH_CHECK("k_wpass_a");
-    { PROF(KID_WB); WLAUNCH(sp, (k_wpass_b<K1>), (k_wpass_b<K1, K1 == 32>), dim3(g.gridS), dim3(NTW), g.ldsWB * 4, s, g,
+    // k_wpass_b keeps nothing in LDS and needs 38 VGPRs at cfg5: two 16-wave workgroups per CU (elementwise,
+    // so the grid does not touch the numerics)
+    { PROF(KID_WB); WLAUNCH(sp, (k_wpass_b<K1>), (k_wpass_b<K1, K1 == 32>), dim3(sp ? std::min(2 * g.gridS, g.B * g.NOC) : g.gridS), dim3(NTW), g.ldsWB * 4, s, g,
                             params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2),
                             (float*)(ws + L.E1), (float*)(ws + L.E2)); } LAUNCH_CHECK("k_wpass_b");
     { PROF(KID_WB2); WLAUNCH(sp, k_wpass_b2<NTB2>, (k_wpass_b2<NTB2, true>), dim3(g.gridW2), dim3(NTB2), g.ldsWB2 * 4, s,

@@ -470,6 +470,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_b(Geo gin, const float* __restric
             for (int m = 0; m < MOW; ++m) {
                 const int oc = lane + 64 * m;
                 if (m < nmo && oc < NO) {
+                    float d2o[2], e1o[2], e2o[2];
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int q = 2 * oc + h;
@@ -483,11 +484,23 @@ __global__ __launch_bounds__(NTW) void k_wpass_b(Geo gin, const float* __restric
                             e1 += dz;
                             e2 = fmaf(dz, xh, e2);
                         }
-                        if (q < T1) {
-                            d2g[rb + q] = pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q));
-                            E1g[rb + q] = e1;
-                            E2g[rb + q] = e2;
+                        d2o[h] = pe * 0.25f * keep_mul(g, mask2, dk0, (unsigned)(rb + q));
+                        e1o[h] = e1;
+                        e2o[h] = e2;
+                    }
+                    // the octet's two pooled samples as one 8-byte store per plane (T1 even: both in
+                    // range or neither), else one store per sample
+                    const int q0 = 2 * oc;
+                    if ((T1 & 1) == 0) {
+                        if (q0 < T1) {
+                            *reinterpret_cast<floatx2*>(d2g + rb + q0) = (floatx2){d2o[0], d2o[1]};
+                            *reinterpret_cast<floatx2*>(E1g + rb + q0) = (floatx2){e1o[0], e1o[1]};
+                            *reinterpret_cast<floatx2*>(E2g + rb + q0) = (floatx2){e2o[0], e2o[1]};
                         }
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h)
+                            if (q0 + h < T1) { d2g[rb + q0 + h] = d2o[h]; E1g[rb + q0 + h] = e1o[h]; E2g[rb + q0 + h] = e2o[h]; }
                     }
                 }
             }
