@@ -115,6 +115,11 @@ def test_flat_layout_follows_replaced_parameters_and_buffers():
     assert torch.equal(m.flat_parameters()[-4:], torch.arange(4, dtype=torch.float32))
     m.aggregation[0].running_var = torch.full((16,), 2.0)
     assert torch.all(m.flat_bn_buffers()[32:48] == 2.0)       # rm1 rv1 (8 each), rm2, rv2 (16 each)
+    # the fused steps' single check (flat_views) sees a rebinding as well
+    m.spatial.weight.data = torch.full_like(m.spatial.weight, -0.5)
+    flat, bn, nbt = m.flat_views()
+    assert torch.all(flat[o:o + 16 * 22] == -0.5) and m.spatial.weight.data_ptr() == flat.data_ptr() + 4 * o
+    assert bn.data_ptr() == m.flat_bn_buffers().data_ptr() and nbt.data_ptr() == m.flat_num_batches_tracked().data_ptr()
 
 
 def test_cpu_tensors_raise_instead_of_falling_back():
