@@ -36,6 +36,12 @@ constexpr int NWB2 = NTB2 / 64;
 #define EEGNET_WD_NT 512
 #endif
 constexpr int NTD5 = EEGNET_WD_NT;
+// x-operand k-groups the cfg5 wide pass E loads per batch for its dws GEMM (A/B builds: 4, the default,
+// two batches of the wave's 8; 6 and 8 -- more of the range in flight before the barrier -- measured
+// slower, k_wpass_e 170-174 -> 175-186 us: profiles/r6zp_ab_xpf.txt)
+#ifndef EEGNET_WE_XPF
+#define EEGNET_WE_XPF 4
+#endif
 constexpr int LQW = 8;                 // left pad of block-2 rows (dw16 reads t-7, its transpose t+7)
 constexpr int KSW = 16;                // spatial GEMM k-steps: C <= 64
 constexpr int MAXNOC = 4;              // o-chunks: F2 <= 64
@@ -1474,7 +1480,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         // This wave's x operand goes out XPF k-groups at a time, the first batch BEFORE the next rows'
         // DMA and the barrier: its latency overlaps the other waves' FIR^T (loaded one k-group per
         // iteration inside the GEMM, every load waited for its own round trip).
-        constexpr int XPF = 4;
+        constexpr int XPF = SPEC ? EEGNET_WE_XPF : 4;
         const int cx = ct * 16 + li;
         const bool bon = cx < C;
         // k permutation of the operands (the same in A and B).  cfg5 (SPEC, T = 512): k-group kg of a
