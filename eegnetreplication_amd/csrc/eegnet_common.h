@@ -144,7 +144,6 @@ __device__ __forceinline__ void trial_range(const Geo& g, int& b0, int& b1) {
     b1 = (int)((w + 1) * g.B / G);
 }
 
-
 // fine stamps of the reduction / finalize critical path (row TR_FINE + pass, slot k), thread 0 only
 constexpr int TR_FINE = 6;
 #define TRACE_FS(g_, pass_, k_)                                                                  \
@@ -223,38 +222,7 @@ struct FinArgs {
     float* adam_v;
     int32_t* step;
     float lr, b1, b2, eps;
-    // the next pass's first-trial rows of this workgroup's trial range (whole-batch launches of the
-    // streaming grid: the next pass runs the same grid, so its workgroup blockIdx.x lands on this XCD):
-    // read into L2 by the workgroups that lose the reduction ticket, after it (l2_warm_next); null = none
-    const float* warm[3];
-    int warm_n[3];                // floats per trial of warm[k]
 };
-
-// EEGNET_L2WARM = 1 (A/B builds; measured neutral -- pass E's prologue did not shorten and pass D's end
-// waited for the loads: profiles/r6ze_ab_l2warm.txt)
-#ifndef EEGNET_L2WARM
-#define EEGNET_L2WARM 0
-#endif
-// read the next pass's first-trial rows of this workgroup's trial range (FinArgs::warm) into this XCD's
-// L2: one 16-byte load per lane per 1 KiB, kept alive by an empty asm use.  Called by the workgroups
-// that lost the reduction ticket, so the winner's reduction and finalize stay the critical path; the
-// next pass's prologue then finds them in L2 instead of HBM.
-__device__ __forceinline__ void l2_warm_next(const Geo& g, const FinArgs& fa) {
-    if (!EEGNET_L2WARM) return;
-    int b0, b1;
-    trial_range(g, b0, b1);
-    if (b0 >= b1) return;
-    float acc = 0.f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        if (!fa.warm[k]) continue;
-        const int n = fa.warm_n[k];
-        const float* p = fa.warm[k] + (size_t)b0 * n;
-        for (int i = 4 * (int)threadIdx.x; i < n; i += 4 * (int)blockDim.x)
-            acc += reinterpret_cast<const floatx4*>(p + i)[0][0];
-    }
-    asm volatile("" :: "v"(acc));
-}
 
 // ticket blocks of the five passes in a workspace
 enum { TK_A = 0, TK_B, TK_C, TK_D, TK_E, TK_COUNT };
@@ -278,9 +246,7 @@ struct FoldCall {
 // each CU ran its last ~20 µs at one workgroup's occupancy.  A workgroup drops a priority level per
 // quarter of its range, so the one ahead yields to the one behind.
 // cache policy of the step's plane stores (A/B build options): 1 = nontemporal (the default), 0 = plain
-// stores, 2 = nontemporal at system scope (sc0 sc1 nt: written through, so no dirty plane lines are
-// left in L2 for the kernel's end-of-launch release).  NT_MID: d2/E1/E2 (pass B, read by D) and dp2
-// (pass D, read by E); NT_SV: s and v (pass A)
+// stores.  NT_MID: d2/E1/E2 (pass B, read by D) and dp2 (pass D, read by E); NT_SV: s and v (pass A)
 #ifndef EEGNET_NT_MID
 #define EEGNET_NT_MID 1
 #endif
@@ -289,16 +255,8 @@ struct FoldCall {
 #endif
 template <int NT, typename V>
 __device__ __forceinline__ void st_pol(V v, V* p) {
-    if constexpr (NT == 2) {
-        if constexpr (sizeof(V) == 16)
-            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" :: "v"(p), "v"(v) : "memory");
-        else
-            asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" :: "v"(p), "v"(v) : "memory");
-    } else if constexpr (NT != 0) {
-        __builtin_nontemporal_store(v, p);
-    } else {
-        *p = v;
-    }
+    if constexpr (NT != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
 }
 
 #ifndef EEGNET_PRIO
@@ -357,8 +315,6 @@ __device__ __forceinline__ FinArgs fold_fin(const FoldCall& fc, const eegnet_fol
     a.adam_v = adam ? f.adam_state + nparam : nullptr;
     a.step = adam ? f.step : nullptr;
     a.lr = fc.lr; a.b1 = fc.b1; a.b2 = fc.b2; a.eps = fc.eps;
-    a.warm[0] = a.warm[1] = a.warm[2] = nullptr;
-    a.warm_n[0] = a.warm_n[1] = a.warm_n[2] = 0;
     return a;
 }
 
@@ -367,14 +323,6 @@ __host__ __device__ constexpr int rup4(int a) { return (a + 3) & ~3; }
 __host__ __device__ constexpr int imax(int a, int b) { return a > b ? a : b; }
 // row pitch of the s plane [B][F2][s_pitch(T)] (floats): T rounded up to 4, so rows are 16-byte units
 __host__ __device__ constexpr int s_pitch(int T) { return (T + 3) & ~3; }
-// EEGNET_NOV = 1: the 22 x 256 EEGNet-8,2 shape keeps no v plane -- pass A stores only s, passes B
-// and E recompute v = FIR(s) from s rows in LDS with pass A's own fir8 (bit-identical v)
-#ifndef EEGNET_NOV
-#define EEGNET_NOV 0
-#endif
-__host__ __device__ constexpr bool nov_shape(int K1, int CC, int TT, int FF) {
-    return EEGNET_NOV && K1 == 32 && CC == 22 && TT == 256 && FF == 16;
-}
 
 __host__ __device__ constexpr int row_stride(int K1, int T) {
     // rows of x / s / dy / e: [LP zeros | T samples | >= R zeros]; long enough for the last 4-output

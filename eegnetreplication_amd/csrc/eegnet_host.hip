@@ -173,8 +173,6 @@ static int make_geo(const eegnet_dims* d, Geo* g, bool launch = true) {
     // the reduction tail and finalize reuse each pass kernel's LDS (doubles = 2 floats)
     auto tail = [](int ncols, int fin) { return 2 * (tail_s_doubles(ncols) + std::max(tail_scratch_doubles(ncols), fin)); };
     g->ldsA = std::max(g->ldsA, tail(g->nA, fin1_scratch_doubles(g->K1, g->F1, g->F2, g->C)));
-    // nov_shape: pass B stages the s rows [F2][RS] it recomputes v from
-    if (nov_shape(g->K1, g->C, g->T, (g->F1 == 8 && g->D == 2) ? 16 : 0)) g->ldsB += g->F2 * g->RS;
     g->ldsB = std::max(g->ldsB, tail(g->nB, 0));
     g->ldsC = std::max(g->ldsC, tail(g->nC, 0));
     g->ldsD = std::max(g->ldsD, tail(g->nD, 0));
@@ -371,7 +369,7 @@ static void ensure_attrs() {
     set_attrs_wide<64>();
     for (const void* f : {(const void*)k_wpass_a<32, true>, (const void*)k_wpass_b<32, true>, (const void*)k_wpass_e<32, true>,
                           (const void*)k_winfer<32, true>, (const void*)k_wpass_b2<NTB2, true>,
-                          (const void*)k_wpass_c<NTB2, false, true>, (const void*)k_wpass_d<NTD5, false, true>,
+                          (const void*)k_wpass_c<NTB2, false, true>, (const void*)k_wpass_d<NTB2, false, true>,
                           (const void*)k_coltail<3, true>, (const void*)k_coltail<4, true>, (const void*)k_coltail<5, true>})
         hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     for (const void* f : {(const void*)k_wpass_b2<NTB2>, (const void*)k_wpass_c<NTB2>, (const void*)k_wpass_d<NTB2>,
@@ -482,7 +480,7 @@ static int run_backward_wide(const Geo& g, const WsLayout& L, char* ws, float* p
                             g, params, coef, (const float*)(ws + L.r3), m3, dlogits, labels, logits, (float*)(ws + L.dl),
                             (float*)(ws + L.partC), c_mode, fc, FoldCall{}); } LAUNCH_CHECK("k_wpass_c(bwd)");
     if (g.splitC) { coltail(3, (const float*)(ws + L.partC), g.gridW2, g.nC, fc, 0); LAUNCH_CHECK("k_coltail(C)"); }
-    { PROF(KID_WD); WLAUNCH(sp, k_wpass_d<NTB2>, (k_wpass_d<NTD5, false, true>), dim3(g.grid), dim3(sp ? NTD5 : NTB2), g.ldsWD * 4, s,
+    { PROF(KID_WD); WLAUNCH(sp, k_wpass_d<NTB2>, (k_wpass_d<NTB2, false, true>), dim3(g.grid), dim3(NTB2), g.ldsWD * 4, s,
                             g, params, coef, (const float*)(ws + L.d2), (const float*)(ws + L.E1), (const float*)(ws + L.E2),
                             (const float*)(ws + L.q3), (const float*)(ws + L.r3), m2, m3, dl,
                             (float*)(ws + L.dp2), (float*)(ws + L.partD), fd, FoldCall{}); }
@@ -505,10 +503,7 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
                        const float* x, const uint8_t* m2, int update_running, int64_t* nbt, hipStream_t s,
                        const FoldCall& fc = FoldCall{}, int nf = 1, int only = -1) {
     if (g.wide) return run_forward_wide<K1>(g, L, ws, params, bn, x, m2, update_running, nbt, s);
-    FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
-    // pass B reads the v plane (the s plane at nov_shape) a trial range per workgroup on the same grid
-    if (nov_shape(g.K1, g.C, g.T, (g.F1 == 8 && g.D == 2) ? 16 : 0)) { fa.warm[0] = (const float*)(ws + L.s); fa.warm_n[0] = g.F2 * s_pitch(g.T); }
-    else { fa.warm[0] = (const float*)(ws + L.v); fa.warm_n[0] = g.F2 * ((g.T + 7) / 8 * 8); }
+    const FinArgs fa = fin_args(L, ws, TK_A, bn, nullptr, nullptr, update_running, 0);
     const FinArgs fb = fin_args(L, ws, TK_B, bn, nullptr, nullptr, update_running, 0, nbt);
 #define LAUNCH_A(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_a<K, CC, TT, FF, true>), dim3(g.gridA, nf), dim3(NTB), g.ldsA * 4, s, \
                                                    g, params, x, (float*)(ws + L.s), (float*)(ws + L.v), (float*)(ws + L.partA), fa, fc); \
@@ -517,11 +512,11 @@ static int run_forward(const Geo& g, const WsLayout& L, char* ws, const float* p
     if (only < 0 || only == 0) { { PROF(KID_A); EEG_DISPATCH(K1, g, LAUNCH_A);
     } LAUNCH_CHECK("k_pass_a"); }
 #define LAUNCH_B(K, CC, TT, FF) if (fc.folds) hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF, true>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
-                       g, params, (const float*)(ws + L.coef), (const float*)(ws + (nov_shape(K, CC, TT, FF) ? L.s : L.v)), m2, (float*)(ws + L.d2), \
+                       g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
                        (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
                        (float*)(ws + L.partB), fb, fc); \
     else hipLaunchKernelGGL((k_pass_b<K, CC, TT, FF>), dim3(g.gridS, nf), dim3(NTB), g.ldsB * 4, s, \
-                       g, params, (const float*)(ws + L.coef), (const float*)(ws + (nov_shape(K, CC, TT, FF) ? L.s : L.v)), m2, (float*)(ws + L.d2), \
+                       g, params, (const float*)(ws + L.coef), (const float*)(ws + L.v), m2, (float*)(ws + L.d2), \
                        (float*)(ws + L.E1), (float*)(ws + L.E2), (float*)(ws + L.q3), (float*)(ws + L.r3), \
                        (float*)(ws + L.partB), fb, fc)
     if (only < 0 || only == 1) { { PROF(KID_B); EEG_DISPATCH(K1, g, LAUNCH_B);
@@ -542,11 +537,7 @@ static int run_backward(const Geo& g, const WsLayout& L, char* ws, float* params
     const float* coef = (const float*)(ws + L.coef);
     const float* dl = dlogits ? dlogits : (const float*)(ws + L.dl);
     const FinArgs fcC = fin_args(L, ws, TK_C, nullptr, grads, loss, 0, (c_mode & PC_CE) ? 1 : 0);
-    FinArgs fd = fin_args(L, ws, TK_D, nullptr, grads, nullptr, 0, 0);
-    // pass E's prologue rows (s, v, dp2 of its first trial) on k_pass_dr's grid, which is pass E's
-    fd.warm[0] = (const float*)(ws + L.s); fd.warm_n[0] = g.F2 * s_pitch(g.T);
-    fd.warm[1] = (const float*)(ws + L.v); fd.warm_n[1] = g.F2 * ((g.T + 7) / 8 * 8);
-    fd.warm[2] = (const float*)(ws + L.dp2); fd.warm_n[2] = g.F2 * g.T1;
+    const FinArgs fd = fin_args(L, ws, TK_D, nullptr, grads, nullptr, 0, 0);
     FinArgs fe = fin_args(L, ws, TK_E, nullptr, grads, nullptr, 0, 0);
     if (adam) {
         fe.params = params; fe.adam_m = adam->adam_m; fe.adam_v = adam->adam_v; fe.step = adam->step;

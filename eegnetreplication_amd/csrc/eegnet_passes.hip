@@ -1075,7 +1075,6 @@ __global__ __launch_bounds__(NTB, TT ? WPEB : 2) void k_pass_dr(Geo g, const flo
     }
     double* dsm = (double*)sm;
     if (grid_reduce(g, part, g.nD, fa, dsm)) { fin4(g, prm, dsm + 2, fa); TRACE(g, 3, TR_FIN); }
-        else if (!FOLD) l2_warm_next(g, fa);          // pass E's first s / v / dp2 rows of this trial range
 }
 
 // ================================================================================================

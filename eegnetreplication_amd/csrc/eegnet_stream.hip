@@ -504,7 +504,6 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
         const int hr = fir_row(lane), o = RPW * wave + hr;
         float* const vrow = vg + ((size_t)b * F2 + (o < F2 ? o : 0)) * (8 * NO);
         constexpr bool DEFER = XDMA;                       // (without DMA the barrier waits for no store)
-        constexpr bool NOVS = nov_shape(K1, CC, TT, FF);   // no v plane: B and E recompute v from s
         constexpr int MOA = DEFER ? EEG_MO(TT) : 1;
         float vs[MOA][8];
         {
@@ -569,7 +568,7 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
         static_assert(NSST <= 16, "vmcnt window");
         if constexpr (XDMA) barrier_vm<NSST>();
         else __syncthreads();                              // Xb staged, Ss free
-        if constexpr (DEFER && !NOVS) {
+        if constexpr (DEFER) {
             if (o < F2) {
 #pragma unroll
                 for (int m = 0; m < MOA; ++m) {
@@ -657,8 +656,6 @@ __device__ __forceinline__ void pass_a_body(const Geo& g, const float* __restric
         if (grid_reduce(g, part, g.nA, fa, dsm)) {
             fin1_body<K1, true>(g, prm, dsm + 2, dsm + tail_s_doubles(g.nA), fa, f1);
             TRACE(g, 0, TR_FIN);
-        } else if (!FOLD) {
-            l2_warm_next(g, fa);                       // pass B's first v rows of this trial range
         }
     }
 }
@@ -803,7 +800,7 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
         char* ws = (char*)f.ws;
         prm = f.params;
         coef = (const float*)(ws + fc.off.coef);
-        vg = (const float*)(ws + (nov_shape(K1, CC, TT, FF) ? fc.off.s : fc.off.v));
+        vg = (const float*)(ws + fc.off.v);
         mask2 = nullptr;
         d2g = (float*)(ws + fc.off.d2); E1g = (float*)(ws + fc.off.E1); E2g = (float*)(ws + fc.off.E2);
         q3g = (float*)(ws + fc.off.q3); r3g = (float*)(ws + fc.off.r3);
@@ -816,12 +813,6 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
     float* D2s = sm;
     float* Qs0 = D2s + F2 * RS2;
     float* Wt = Qs0 + 2 * F2 * RS2;    // block-2 weights, read with wave-uniform addresses
-    // nov_shape: vg is the s plane; each wave stages its own s rows here and recomputes v = FIR(s)
-    // exactly as pass A did (fir8 over the same LDS row layout: bit-identical v)
-    constexpr bool NOVS = nov_shape(K1, CC, TT, FF);
-    static_assert(!NOVS || s_pitch(TT) == 8 * EEG_NO(TT), "s rows load as v octets");
-    float* const Sw = Wt + F2MAX * (K2 + F2MAX);
-    using G_ = KG<K1>;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int b0, b1;
@@ -834,13 +825,8 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
     constexpr bool VPF = TT != 0;
     float vpf[MO][8];
     if (VPF && b0 < b1) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
-    constexpr int NTS = FF ? 1 : RPW;
-    float tap[NOVS ? NTS : 1][NOVS ? K1 : 1];
-    if constexpr (NOVS) load_taps<K1, NTS>(g, prm, FF ? 2 : g.D, F2, wave, tap);
 
     for (int i = tid; i < 3 * F2 * RS2; i += NTB) sm[i] = 0.f;     // pads stay zero
-    if constexpr (NOVS)
-        for (int i = tid; i < F2 * RS; i += NTB) Sw[i] = 0.f;       // s rows: pads stay zero
     for (int i = tid; i < F2MAX * (K2 + F2MAX); i += NTB) {
         float v = 0.f;
         if (i < F2MAX * K2) { if (i < F2 * K2) v = prm[g.o_w2 + i]; }
@@ -878,28 +864,6 @@ __device__ __forceinline__ void pass_b_body(const Geo& g, const float* __restric
             if (bn < b1) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
         } else {
             v_load<MO>(vg, b, F2, NO, oh, lane, vc);
-        }
-        if constexpr (NOVS) {
-            // vc holds this lane's s octets: into the wave's own LDS rows, then v = FIR(s) per octet
-            if (oh < F2) {
-#pragma unroll
-                for (int m = 0; m < MO; ++m) {
-                    const int oc = fir_oct(lane) + 32 * m;
-                    if (oc < NO)
-                        lds_st_oct(Sw + oh * RS + LP + 8 * oc, oc, (floatx4){vc[m][0], vc[m][1], vc[m][2], vc[m][3]},
-                                   (floatx4){vc[m][4], vc[m][5], vc[m][6], vc[m][7]});
-                }
-            }
-            wave_lds_fence();
-            float tl[K1];
-            half_taps<K1, NTS>(tap, hr, tl);
-#pragma unroll
-            for (int m = 0; m < MO; ++m) {
-                const int oc = min(fir_oct(lane) + 32 * m, NO - 1);
-                float w[4 * G_::NW8];
-                lds_window<G_::NW8>(Sw + min(oh, F2 - 1) * RS + 8 * oc, w);
-                fir8<K1, G_::OFF>(w, tl, vc[m]);
-            }
         }
         TRACE_PH(g, 1, 0, tph_);
         // BN2, ELU, pool4, dropout (model.py:47-50) of this lane's octets
@@ -1036,11 +1000,6 @@ __global__ __launch_bounds__(NTB, WPEB) void k_pass_b(Geo g, const float* __rest
 #ifndef EEGNET_LDSX_E
 #define EEGNET_LDSX_E 0
 #endif
-// EEGNET_E_XTOP = 1 (A/B builds): the pipelined shape (PIPEE) issues the trial's x DMA at the top of
-// the trial, right after the previous closing barrier freed the x buffer, instead of after dy2
-#ifndef EEGNET_E_XTOP
-#define EEGNET_E_XTOP 0
-#endif
 template <int K1, int CC, int TT, int FF, bool FOLD>
 __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   // Adam (finalize) writes it
                                             const float* coef,    // the finalize writes it: no __restrict__
@@ -1104,10 +1063,6 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
     // trial's dp2 (right after its dy2 phase) and s (right after its lag correlation), the next v is
     // loaded a whole trial ahead, and the first barrier waits only for this trial's x
     constexpr bool PIPEE = ONEOC && XDMA_ && DPDMA_ && (TT / 4 == 64) && (TT == 256);
-    // nov_shape: no v plane -- v = FIR(s) of this wave's own s rows at the top of each trial (the rows
-    // landed by the previous closing barrier), pass A's fir8 on the same LDS row layout (bit-identical)
-    constexpr bool NOVS = nov_shape(K1, CC, TT, FF);
-    static_assert(!NOVS || PIPEE, "the v recompute relies on the pipelined s-row DMA");
     float sdyl = 0.f, sdyvl = 0.f;                   // this lane's row (half-wave) sums of dy, dy v
     // dW1 lag correlation Q[o][k] = sum_t dy[o][t] s[o][t+k-P] on the matrix cores.  With t = 16a + u
     // and s'[i] = s[i-P]:
@@ -1181,7 +1136,7 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
                 if (tid + NTB * j < ndp) DP[tid + NTB * j] = pdp[j];
             for (int i = tid + NTB * NDP; i < ndp; i += NTB) DP[i] = dp2g[(size_t)b0 * ndp + i];
         }
-        if constexpr (VPF && !NOVS) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
+        if constexpr (VPF) v_load<MO>(vg, b0, F2, NO, oh, lane, vpf);
         TRACE_PS(g, 4);
     }
     if constexpr (XDMA) zero_pads(sm, 2 * F2 + C, RS, LP, T, tid);   // the data windows are DMA'd / written
@@ -1222,24 +1177,8 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
     for (int b = b0; b < b1; ++b) {
         const int bn = b + 1;
         pace_prio(b - b0, b1 - b0);
-        if constexpr (PIPEE && EEGNET_E_XTOP) {
-            // vmcnt is 0 here (the previous closing barrier); the explicit wait tells the compiler so,
-            // or its wait for vpf at the first use would count this asm DMA as older work
-            __builtin_amdgcn_s_waitcnt(0);
-            if (EEGNET_LDSX_E != 7) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
-        }
         float vc[MO][8];
-        if constexpr (NOVS) {
-            float tl[K1];
-            half_taps<K1, NTS>(tap, hr, tl);
-#pragma unroll
-            for (int m = 0; m < MO; ++m) {
-                const int oc = min(fir_oct(lane) + 32 * m, NO - 1);
-                float w[4 * G_::NW8];
-                lds_window<G_::NW8>(Ss + min(oh, F2 - 1) * RS + 8 * oc, w);
-                fir8<K1, G_::OFF>(w, tl, vc[m]);
-            }
-        } else if constexpr (VPF) {
+        if constexpr (VPF) {
 #pragma unroll
             for (int m = 0; m < MO; ++m)
 #pragma unroll
@@ -1295,7 +1234,7 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
         }
         // this trial's x rows for the dws GEMM (the buffer was last read by the previous trial's
         // GEMM); they land during the lag correlation / FIR^T, by the next barrier
-        if constexpr (XDMA && !(PIPEE && EEGNET_E_XTOP))
+        if constexpr (XDMA)
             if (EEGNET_LDSX_E != 7) x_dma_asm(x + fold_row(perm, row0, b) * (C * XP), C, T, XP, RS, LP, Xb, wave, lane);
         TRACE_PH(g, 4, 2, tph_);
         {
@@ -1455,7 +1394,7 @@ __device__ __forceinline__ void pass_e_body(const Geo& g, const float* prm,   //
             }
             if constexpr (DPDMA) flat_dma_asm(dp2g + (size_t)bn * ndp, ndp, DP, wave, lane);
             asm volatile("" ::: "memory");                 // the v loads issue after the DMA (barrier_vm)
-            if constexpr (VPF && !NOVS) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
+            if constexpr (VPF) v_load<MO>(vg, bn, F2, NO, oh, lane, vpf);
         }
         TRACE_PH(g, 4, 5, tph_);
         // Xm[o][c] += sum_t e[o][t] x[c][t] on the matrix cores (16 e rows x 16 x rows of this wave's

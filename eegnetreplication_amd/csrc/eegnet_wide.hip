@@ -30,18 +30,6 @@ constexpr int NTW = 1024;              // threads of the wide streaming passes a
 constexpr int NWW = NTW / 64;          // = 16 rows of an o-chunk, one per wave
 constexpr int NTB2 = 512;              // threads of the wide block-2 passes (8 waves)
 constexpr int NWB2 = NTB2 / 64;
-// threads of the cfg5 (SPEC) wide pass D: 512 (one 8-wave workgroup per CU, 255 VGPRs) or, A/B builds
-// -DEEGNET_WD_NT=1024, 16 waves per CU at <= 128 VGPRs
-#ifndef EEGNET_WD_NT
-#define EEGNET_WD_NT 512
-#endif
-constexpr int NTD5 = EEGNET_WD_NT;
-// x-operand k-groups the cfg5 wide pass E loads per batch for its dws GEMM (A/B builds: 4, the default,
-// two batches of the wave's 8; 6 and 8 -- more of the range in flight before the barrier -- measured
-// slower, k_wpass_e 170-174 -> 175-186 us: profiles/r6zp_ab_xpf.txt)
-#ifndef EEGNET_WE_XPF
-#define EEGNET_WE_XPF 4
-#endif
 constexpr int LQW = 8;                 // left pad of block-2 rows (dw16 reads t-7, its transpose t+7)
 constexpr int KSW = 16;                // spatial GEMM k-steps: C <= 64
 constexpr int MAXNOC = 4;              // o-chunks: F2 <= 64
@@ -1004,7 +992,7 @@ __global__ __launch_bounds__(NT, (SPEC && NT == 512) ? 4 : 1) void k_wpass_c(Geo
 // LDS: D2 [F2P][RB] | Q [F2P][RB] (q, then dq) | DR [F2P][RB] | W2s | Hd [NF] | item sums
 // ================================================================================================
 template <int NT, bool FOLD = false, bool SPEC = false>
-__global__ __launch_bounds__(NT, NT == 1024 ? 4 : 2) void k_wpass_d(Geo gin, const float* __restrict__ prm, const float* coef,
+__global__ __launch_bounds__(NT, 2) void k_wpass_d(Geo gin, const float* __restrict__ prm, const float* coef,
                                                   const float* __restrict__ d2g, const float* __restrict__ E1g,
                                                   const float* __restrict__ E2g, const float* __restrict__ q3g,
                                                   const float* __restrict__ r3g, const uint8_t* __restrict__ mask2,
@@ -1078,8 +1066,8 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : 2) void k_wpass_d(Geo gin, con
     // per thread and plane, loaded into registers a whole trial ahead and stored to LDS at the top of
     // the trial; the dd2 phase loads its items' E1 / E2 two items at a time (each of the four items
     // waited one global round trip for them; all four at once, or from the top of the trial, spill)
-    constexpr bool PFD = SPEC && (NT == 512 || NT == 1024);
-    constexpr int NPD = 2048 / NT;                     // float4 per thread and plane at cfg5
+    constexpr bool PFD = SPEC && NT == 512;
+    constexpr int NPD = 4;                             // float4 per thread and plane at cfg5
     floatx4 pd[PFD ? 3 : 1][PFD ? NPD : 1], pe1[PFD ? NPD : 1], pe2[PFD ? NPD : 1];
     auto planes_load = [&](int bb) {
         if constexpr (PFD) {               // (the only caller; keeps the 1 x 1 arrays of !PFD unindexed)
@@ -1223,7 +1211,6 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : 2) void k_wpass_d(Geo gin, con
             IS[nit + it] += s2;
         };
         if constexpr (PFD) {
-            static_assert(NPD % 2 == 0, "two dd2 items per round trip");
 #pragma unroll
             for (int h = 0; h < NPD; h += 2) {         // two items' E1 / E2 per round trip
 #pragma unroll
@@ -1480,7 +1467,7 @@ __global__ __launch_bounds__(NTW) void k_wpass_e(Geo gin, const float* prm, cons
         // This wave's x operand goes out XPF k-groups at a time, the first batch BEFORE the next rows'
         // DMA and the barrier: its latency overlaps the other waves' FIR^T (loaded one k-group per
         // iteration inside the GEMM, every load waited for its own round trip).
-        constexpr int XPF = SPEC ? EEGNET_WE_XPF : 4;
+        constexpr int XPF = 4;
         const int cx = ct * 16 + li;
         const bool bon = cx < C;
         // k permutation of the operands (the same in A and B).  cfg5 (SPEC, T = 512): k-group kg of a
