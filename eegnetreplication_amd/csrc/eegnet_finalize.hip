@@ -68,6 +68,21 @@ constexpr long long FLAT_ELEMS = 16384;   // partial-row elements (grid x ncols)
 #endif
 __host__ __device__ constexpr int tail_s_doubles(int ncols) { return 2 + ((ncols + 1) & ~1); }
 
+// copy n published doubles into LDS, NLB loads in flight per thread (a one-load-per-iteration loop
+// waits a global round trip per iteration: k_coltail's 4-6 K totals at cfg5)
+template <int NLB>
+__device__ __forceinline__ void stage_pub(double* dst, const double* src, int n) {
+    const int nth = blockDim.x;
+    for (int i0 = threadIdx.x; i0 < n; i0 += NLB * nth) {
+        double v[NLB];
+#pragma unroll
+        for (int j = 0; j < NLB; ++j) v[j] = ld_pub(src + min(i0 + j * nth, n - 1));
+#pragma unroll
+        for (int j = 0; j < NLB; ++j)
+            if (i0 + j * nth < n) dst[i0 + j * nth] = v[j];
+    }
+}
+
 __device__ bool grid_reduce(const Geo& g, const float* part, int ncols, const FinArgs& fa, double* dsm) {
     const int tid = threadIdx.x, nth = blockDim.x;
     int* flag = (int*)dsm;
@@ -697,7 +712,7 @@ __device__ __forceinline__ void fin5(const Geo& g, const float* prm, const doubl
 __global__ __launch_bounds__(512) void k_fin(Geo g, const float* prm, FinArgs fa, int pass, int ncols) {
     extern __shared__ __attribute__((aligned(16))) double dfin[];
     double* S = dfin + 2;
-    for (int c = threadIdx.x; c < ncols; c += blockDim.x) S[c] = fa.part2[c];
+    stage_pub<8>(S, fa.part2, ncols);
     __syncthreads();
     double* scr = dfin + tail_s_doubles(ncols);
     switch (pass) {
@@ -747,7 +762,7 @@ __global__ __launch_bounds__(NTCT) void k_coltail(Geo gin, const float* prm, con
     }
     if (!take_ticket(fa.cnt + (NCNT - 1), gridDim.x, (int*)dsmt)) return;
     double* S = dsmt + 2;
-    for (int i = tid; i < ncols; i += NTCT) S[i] = ld_pub(fa.part2 + i);
+    stage_pub<8>(S, fa.part2, ncols);
     if (tid == 0) __hip_atomic_store(fa.cnt + (NCNT - 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if constexpr (FIN == 3) fin3(g, prm, S, fa);
